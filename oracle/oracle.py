@@ -1,0 +1,182 @@
+"""ORACLE -- test infrastructure only.
+
+ctypes wrapper around ``oracle/_build/libtmfwm_oracle.so`` (the plain-C
+restatement in ``tmfwm_oracle.c`` of /root/reference/modules/watermarking.py).
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s
+``cpu_baseline`` leg import this module, and only as the checker / CPU
+baseline.  The product package ``thatsmyface_amd`` never imports it.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "_build", "libtmfwm_oracle.so")
+_lib = None
+
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_f32p = ctypes.POINTER(ctypes.c_float)
+_i32p = ctypes.POINTER(ctypes.c_int32)
+
+
+def build(force: bool = False) -> str:
+    """Compile the oracle with its Makefile (gcc); returns the .so path."""
+    if force or not os.path.exists(_LIB_PATH) or (
+        os.path.getmtime(_LIB_PATH) < os.path.getmtime(os.path.join(_HERE, "tmfwm_oracle.c"))
+    ):
+        subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = ctypes.CDLL(_LIB_PATH)
+        I64, I32, D = ctypes.c_int64, ctypes.c_int, ctypes.c_double
+        sig = {
+            "orc_rgb_to_ycbcr": (None, [_u8p, I64, _f32p]),
+            "orc_ycbcr_to_rgb": (None, [_f32p, I64, _u8p]),
+            "orc_dct2d_blocks": (None, [_f32p, I64, I32, I32]),
+            "orc_dct_rows": (None, [_f32p, I64, I32, I32]),
+            "orc_svd_blocks": (I32, [_f32p, I64, I32, _f32p, _f32p, _f32p, _i32p]),
+            "orc_sigma1_block": (ctypes.c_float, [_f32p, I32]),
+            "orc_blend_reconstruct": (None, [_f32p, _f32p, _f32p, I32, ctypes.c_uint8, D, _f32p]),
+            "orc_gather_blocks": (None, [_f32p, I32, I32, I32, _f32p]),
+            "orc_scatter_blocks": (None, [_f32p, I32, I32, I32, _f32p]),
+            "orc_embed_frame": (I32, [_u8p, I32, I32, _u8p, I32, D, _u8p, I32]),
+            "orc_extract_frame": (I32, [_u8p, _u8p, I32, I32, I32, D, _u8p, I32]),
+            "orc_embed_batch": (I32, [_u8p, I64, I32, I32, _u8p, I32, D, _u8p, I32]),
+            "orc_extract_batch": (I32, [_u8p, _u8p, I64, I32, I32, I32, D, _u8p, I32]),
+            "orc_synth_bytes": (None, [ctypes.c_uint64, I64, I64, I64, _u8p]),
+        }
+        for name, (res, args) in sig.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _p(a: np.ndarray, typ):
+    assert a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(typ)
+
+
+def default_threads() -> int:
+    try:
+        return max(1, len(os.sched_getaffinity(0)))
+    except AttributeError:  # pragma: no cover
+        return os.cpu_count() or 1
+
+
+# --- stages ---------------------------------------------------------------
+def rgb_to_ycbcr(rgb: np.ndarray) -> np.ndarray:
+    rgb = np.ascontiguousarray(rgb, dtype=np.uint8)
+    out = np.empty(rgb.shape[:-1] + (3,), np.float32)
+    lib().orc_rgb_to_ycbcr(_p(rgb, _u8p), rgb.size // 3, _p(out, _f32p))
+    return out
+
+
+def ycbcr_to_rgb(ycc: np.ndarray) -> np.ndarray:
+    ycc = np.ascontiguousarray(ycc, dtype=np.float32)
+    out = np.empty(ycc.shape, np.uint8)
+    lib().orc_ycbcr_to_rgb(_p(ycc, _f32p), ycc.size // 3, _p(out, _u8p))
+    return out
+
+
+def dct_rows(x: np.ndarray, inverse: bool = False) -> np.ndarray:
+    x = np.array(x, dtype=np.float32, order="C", copy=True)
+    n = x.shape[-1]
+    lib().orc_dct_rows(_p(x, _f32p), x.size // n, n, int(inverse))
+    return x
+
+
+def dct2d_blocks(blocks: np.ndarray, inverse: bool = False) -> np.ndarray:
+    x = np.array(blocks, dtype=np.float32, order="C", copy=True)
+    b = x.shape[-1]
+    lib().orc_dct2d_blocks(_p(x, _f32p), x.size // (b * b), b, int(inverse))
+    return x
+
+
+def svd_blocks(D: np.ndarray):
+    D = np.ascontiguousarray(D, dtype=np.float32)
+    b = D.shape[-1]
+    nb = D.size // (b * b)
+    U = np.empty(D.shape, np.float32)
+    Vt = np.empty(D.shape, np.float32)
+    S = np.empty(D.shape[:-1], np.float32)
+    sw = np.empty(max(nb, 1), np.int32)
+    lib().orc_svd_blocks(_p(D, _f32p), nb, b, _p(U, _f32p), _p(S, _f32p), _p(Vt, _f32p), _p(sw, _i32p))
+    return U, S, Vt, sw[:nb]
+
+
+def sigma1(D: np.ndarray) -> float:
+    D = np.ascontiguousarray(D, dtype=np.float32)
+    return float(lib().orc_sigma1_block(_p(D, _f32p), D.shape[-1]))
+
+
+def blend_reconstruct(U, S, Vt, w: int, alpha: float) -> np.ndarray:
+    U = np.ascontiguousarray(U, np.float32)
+    S = np.ascontiguousarray(S, np.float32)
+    Vt = np.ascontiguousarray(Vt, np.float32)
+    M = np.empty_like(U)
+    lib().orc_blend_reconstruct(_p(U, _f32p), _p(S, _f32p), _p(Vt, _f32p), U.shape[-1], int(w), float(alpha), _p(M, _f32p))
+    return M
+
+
+# --- whole-frame paths ------------------------------------------------------
+def embed_frame(rgb: np.ndarray, wm_tile: np.ndarray, block: int, alpha: float, nthreads: int | None = None) -> np.ndarray:
+    rgb = np.ascontiguousarray(rgb, dtype=np.uint8)
+    H, W = rgb.shape[:2]
+    wm_tile = np.ascontiguousarray(wm_tile, dtype=np.uint8)
+    assert wm_tile.shape == (H // block, W // block), (wm_tile.shape, H, W, block)
+    out = np.empty_like(rgb)
+    rc = lib().orc_embed_frame(_p(rgb, _u8p), H, W, _p(wm_tile, _u8p), block, float(alpha), _p(out, _u8p), nthreads or default_threads())
+    if rc:
+        raise ValueError(f"oracle embed failed rc={rc}")
+    return out
+
+
+def extract_frame(wrgb: np.ndarray, orgb: np.ndarray, block: int, alpha: float, nthreads: int | None = None) -> np.ndarray:
+    wrgb = np.ascontiguousarray(wrgb, dtype=np.uint8)
+    orgb = np.ascontiguousarray(orgb, dtype=np.uint8)
+    H, W = wrgb.shape[:2]
+    assert orgb.shape == wrgb.shape
+    out = np.empty((H // block, W // block), np.uint8)
+    rc = lib().orc_extract_frame(_p(wrgb, _u8p), _p(orgb, _u8p), H, W, block, float(alpha), _p(out, _u8p), nthreads or default_threads())
+    if rc:
+        raise ValueError(f"oracle extract failed rc={rc}")
+    return out
+
+
+def embed_batch(rgb: np.ndarray, wm_tile: np.ndarray, block: int, alpha: float, nthreads: int | None = None) -> np.ndarray:
+    rgb = np.ascontiguousarray(rgb, dtype=np.uint8)
+    n, H, W = rgb.shape[:3]
+    wm_tile = np.ascontiguousarray(wm_tile, dtype=np.uint8)
+    out = np.empty_like(rgb)
+    rc = lib().orc_embed_batch(_p(rgb, _u8p), n, H, W, _p(wm_tile, _u8p), block, float(alpha), _p(out, _u8p), nthreads or default_threads())
+    if rc:
+        raise ValueError(f"oracle embed failed rc={rc}")
+    return out
+
+
+def extract_batch(wrgb: np.ndarray, orgb: np.ndarray, block: int, alpha: float, nthreads: int | None = None) -> np.ndarray:
+    wrgb = np.ascontiguousarray(wrgb, dtype=np.uint8)
+    orgb = np.ascontiguousarray(orgb, dtype=np.uint8)
+    n, H, W = wrgb.shape[:3]
+    out = np.empty((n, H // block, W // block), np.uint8)
+    rc = lib().orc_extract_batch(_p(wrgb, _u8p), _p(orgb, _u8p), n, H, W, block, float(alpha), _p(out, _u8p), nthreads or default_threads())
+    if rc:
+        raise ValueError(f"oracle extract failed rc={rc}")
+    return out
+
+
+def synth_bytes(seed: int, frame0: int, nframes: int, frame_bytes: int) -> np.ndarray:
+    out = np.empty(nframes * frame_bytes, np.uint8)
+    lib().orc_synth_bytes(ctypes.c_uint64(seed), frame0, nframes, frame_bytes, _p(out, _u8p))
+    return out

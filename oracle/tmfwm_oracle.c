@@ -1,0 +1,718 @@
+/*
+ * ORACLE -- TEST INFRASTRUCTURE ONLY.
+ *
+ * Plain-C restatement of the arithmetic of the reference watermark path,
+ * /root/reference/modules/watermarking.py (embed_watermark :135-221,
+ * extract_watermark :224-294) and of the third-party kernels it calls
+ * (scipy 1.15.3 pocketfft DCT-II/III in fp32, numpy 2.2.6 -> LAPACK dgesdd on
+ * an f64 upcast, OpenBLAS 0.3.29 dgemv / sgemm FMA patterns).  The numerical
+ * contract it follows is SURVEY.md section 8(a) N1-N10 and DESIGN.md section 3.
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load
+ * this library, and only as the checker / CPU baseline.  The product path
+ * (thatsmyface_amd/, libtmfwm.so) never links or calls it.
+ *
+ * Parity pinning: tests/golden fixtures were produced by importing the reference
+ * itself (tests/golden/gen_golden.py); tests/test_oracle_golden.py checks this
+ * file against every fixture and against the survey's known-answer hashes.
+ *
+ * SVD: the reference's numbers come from f32(dgesdd(f64(D))).  LAPACK itself is
+ * not restated; any f64-accurate SVD rounded to f32 reproduces it.
+ * The SVD below is a fully specified one-sided (Hestenes) Jacobi in f64 whose
+ * every rounding step is fixed so that the HIP kernels
+ * reproduce it bit for bit.  Its agreement with LAPACK is pinned by the golden
+ * fixtures and measured at scale by tests/test_oracle_vs_lapack.py.
+ *
+ * Build: oracle/Makefile (gcc -O2 -ffp-contract=off, no fast-math).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define ORC_MAXB 16
+
+/* ------------------------------------------------------------------------ */
+/* N1 / N2: RGB -> YCbCr (watermarking.py:23-50)                            */
+/* ------------------------------------------------------------------------ */
+
+/* watermarking.py:29  np.array(img, float32) / 255.0 -> IEEE fp32 divide */
+static inline float unit_from_u8(unsigned v) { return (float)v / 255.0f; }
+
+/* watermarking.py:37-48.  np.dot(f64 3x3, f32 3-vector) runs OpenBLAS dgemv;
+ * its SkylakeX tail evaluates row c as fma(T[c][2], b, fma(T[c][0], r, T[c][1]*g))
+ * (exhaustively verified over 2^24 colours).  The f64 result is
+ * stored into a float32 array; Cb, Cr then get "+= 0.5" in f32 (:48). */
+static inline void colour_fwd(unsigned R, unsigned G, unsigned B, float *y, float *cb, float *cr)
+{
+    const double r = unit_from_u8(R), g = unit_from_u8(G), b = unit_from_u8(B);
+    *y = (float)fma(0.114, b, fma(0.299, r, 0.587 * g));
+    *cb = (float)fma(0.5, b, fma(-0.169, r, -0.331 * g)) + 0.5f;
+    *cr = (float)fma(-0.081, b, fma(0.5, r, -0.419 * g)) + 0.5f;
+}
+
+/* ------------------------------------------------------------------------ */
+/* N9: YCbCr -> RGB (watermarking.py:53-73)                                 */
+/* ------------------------------------------------------------------------ */
+static inline uint8_t u8_from_unit(float f)
+{
+    /* :70 np.clip(rgb, 0, 1) (f32), :73 (rgb * 255).astype(uint8) (f32 multiply, truncation) */
+    if (f < 0.0f) f = 0.0f;
+    if (f > 1.0f) f = 1.0f;
+    return (uint8_t)(f * 255.0f);
+}
+
+static inline void colour_inv(float y, float cbs, float crs, uint8_t out[3])
+{
+    /* :58 Cb, Cr -= 0.5 in f32; :61-67 dgemv with Ti = [[1,0,1.403],[1,-0.344,-0.714],[1,1.773,0]] */
+    const float cbp = cbs - 0.5f, crp = crs - 0.5f;
+    const double Y = y, CB = cbp, CR = crp;
+    out[0] = u8_from_unit((float)fma(1.403, CR, fma(1.0, Y, 0.0 * CB)));
+    out[1] = u8_from_unit((float)fma(-0.714, CR, fma(1.0, Y, -0.344 * CB)));
+    out[2] = u8_from_unit((float)fma(0.0, CR, fma(1.0, Y, 1.773 * CB)));
+}
+
+/* ------------------------------------------------------------------------ */
+/* N3: pocketfft fp32 DCT-II / DCT-III (ortho), lengths 4, 8, 16             */
+/* scipy.fftpack.dct/idct -> pocketfft T_dcst23::exec around rfftp.          */
+/* Every statement below is one fp32 operation (no contraction).             */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+    int n;
+    int nf;
+    int fct[4];            /* rfftp factor list, factor 2 first (pocketfft factorize) */
+    float tw[4][3 * 16];   /* rfftp twiddles per factor: tw[k][(j-1)*(ido-1) + 2i-2 / 2i-1] */
+    float dtw[16];         /* DCT twiddle[i] = cos(2 pi (i+1) / (4n)) */
+    float norm;            /* f32(1/sqrt(2n)) (scipy norm_fct, ortho) */
+} dct_plan;
+
+static dct_plan g_plans[3];
+static int g_plans_ready = 0;
+
+static void plan_init(dct_plan *p, int n)
+{
+    memset(p, 0, sizeof(*p));
+    p->n = n;
+    int len = n, nf = 0;
+    while (len % 4 == 0) { p->fct[nf++] = 4; len >>= 2; }
+    if (len % 2 == 0) {
+        len >>= 1;
+        p->fct[nf++] = 2;
+        int t = p->fct[0]; p->fct[0] = p->fct[nf - 1]; p->fct[nf - 1] = t;
+    }
+    p->nf = nf;
+    /* comp_twiddle: twid[m] = (cos 2 pi m / n, sin 2 pi m / n), computed in high precision */
+    int l1 = 1;
+    for (int k = 0; k < nf; ++k) {
+        int ip = p->fct[k], ido = n / (l1 * ip);
+        if (k < nf - 1) {
+            for (int j = 1; j < ip; ++j)
+                for (int i = 1; i <= (ido - 1) / 2; ++i) {
+                    long double ang = 2.0L * 3.141592653589793238462643383279502884L * (long double)(j * l1 * i) / (long double)n;
+                    p->tw[k][(j - 1) * (ido - 1) + 2 * i - 2] = (float)(double)cosl(ang);
+                    p->tw[k][(j - 1) * (ido - 1) + 2 * i - 1] = (float)(double)sinl(ang);
+                }
+        }
+        l1 *= ip;
+    }
+    for (int i = 0; i < n; ++i) {
+        long double ang = 2.0L * 3.141592653589793238462643383279502884L * (long double)(i + 1) / (long double)(4 * n);
+        p->dtw[i] = (float)(double)cosl(ang);
+    }
+    p->norm = (float)(1.0L / sqrtl((long double)(2 * n)));
+}
+
+static void plans_init(void)
+{
+    if (g_plans_ready) return;
+    plan_init(&g_plans[0], 4);
+    plan_init(&g_plans[1], 8);
+    plan_init(&g_plans[2], 16);
+    g_plans_ready = 1;
+}
+
+static const dct_plan *plan_for(int n)
+{
+    plans_init();
+    return n == 4 ? &g_plans[0] : n == 8 ? &g_plans[1] : &g_plans[2];
+}
+
+#define PM(a, b, c, d) do { float c_ = (c), d_ = (d); (a) = c_ + d_; (b) = c_ - d_; } while (0)
+#define MULPM(a, b, c, d, e, f) do { float c_ = (c), d_ = (d), e_ = (e), f_ = (f); (a) = c_ * e_ + d_ * f_; (b) = c_ * f_ - d_ * e_; } while (0)
+
+static const float SQRT2F = 1.41421356237309504880f;
+static const float HSQT2F = 0.70710678118654752440f;
+
+/* backward radix 2 */
+static void radb2(int ido, int l1, const float *cc, float *ch, const float *wa)
+{
+#define CC(a, b, c) cc[(a) + ido * ((b) + 2 * (c))]
+#define CH(a, b, c) ch[(a) + ido * ((b) + l1 * (c))]
+#define WA(x, i) wa[(i) + (x) * (ido - 1)]
+    for (int k = 0; k < l1; k++) PM(CH(0, k, 0), CH(0, k, 1), CC(0, 0, k), CC(ido - 1, 1, k));
+    if ((ido & 1) == 0)
+        for (int k = 0; k < l1; k++) {
+            CH(ido - 1, k, 0) = 2.0f * CC(ido - 1, 0, k);
+            CH(ido - 1, k, 1) = -2.0f * CC(0, 1, k);
+        }
+    if (ido <= 2) return;
+    for (int k = 0; k < l1; ++k)
+        for (int i = 2; i < ido; i += 2) {
+            int ic = ido - i;
+            float ti2, tr2;
+            PM(CH(i - 1, k, 0), tr2, CC(i - 1, 0, k), CC(ic - 1, 1, k));
+            PM(ti2, CH(i, k, 0), CC(i, 0, k), CC(ic, 1, k));
+            MULPM(CH(i, k, 1), CH(i - 1, k, 1), WA(0, i - 2), WA(0, i - 1), ti2, tr2);
+        }
+#undef CC
+#undef CH
+#undef WA
+}
+
+/* backward radix 4 */
+static void radb4(int ido, int l1, const float *cc, float *ch, const float *wa)
+{
+#define CC(a, b, c) cc[(a) + ido * ((b) + 4 * (c))]
+#define CH(a, b, c) ch[(a) + ido * ((b) + l1 * (c))]
+#define WA(x, i) wa[(i) + (x) * (ido - 1)]
+    for (int k = 0; k < l1; k++) {
+        float tr1, tr2;
+        PM(tr2, tr1, CC(0, 0, k), CC(ido - 1, 3, k));
+        float tr3 = 2.0f * CC(ido - 1, 1, k);
+        float tr4 = 2.0f * CC(0, 2, k);
+        PM(CH(0, k, 0), CH(0, k, 2), tr2, tr3);
+        PM(CH(0, k, 3), CH(0, k, 1), tr1, tr4);
+    }
+    if ((ido & 1) == 0)
+        for (int k = 0; k < l1; k++) {
+            float tr1, tr2, ti1, ti2;
+            PM(ti1, ti2, CC(0, 3, k), CC(0, 1, k));
+            PM(tr2, tr1, CC(ido - 1, 0, k), CC(ido - 1, 2, k));
+            CH(ido - 1, k, 0) = tr2 + tr2;
+            CH(ido - 1, k, 1) = SQRT2F * (tr1 - ti1);
+            CH(ido - 1, k, 2) = ti2 + ti2;
+            CH(ido - 1, k, 3) = -SQRT2F * (tr1 + ti1);
+        }
+    if (ido <= 2) return;
+    for (int k = 0; k < l1; ++k)
+        for (int i = 2; i < ido; i += 2) {
+            float ci2, ci3, ci4, cr2, cr3, cr4, ti1, ti2, ti3, ti4, tr1, tr2, tr3, tr4;
+            int ic = ido - i;
+            PM(tr2, tr1, CC(i - 1, 0, k), CC(ic - 1, 3, k));
+            PM(ti1, ti2, CC(i, 0, k), CC(ic, 3, k));
+            PM(tr4, ti3, CC(i, 2, k), CC(ic, 1, k));
+            PM(tr3, ti4, CC(i - 1, 2, k), CC(ic - 1, 1, k));
+            PM(CH(i - 1, k, 0), cr3, tr2, tr3);
+            PM(CH(i, k, 0), ci3, ti2, ti3);
+            PM(cr4, cr2, tr1, tr4);
+            PM(ci2, ci4, ti1, ti4);
+            MULPM(CH(i, k, 1), CH(i - 1, k, 1), WA(0, i - 2), WA(0, i - 1), ci2, cr2);
+            MULPM(CH(i, k, 2), CH(i - 1, k, 2), WA(1, i - 2), WA(1, i - 1), ci3, cr3);
+            MULPM(CH(i, k, 3), CH(i - 1, k, 3), WA(2, i - 2), WA(2, i - 1), ci4, cr4);
+        }
+#undef CC
+#undef CH
+#undef WA
+}
+
+/* forward radix 2 */
+static void radf2(int ido, int l1, const float *cc, float *ch, const float *wa)
+{
+#define CC(a, b, c) cc[(a) + ido * ((b) + l1 * (c))]
+#define CH(a, b, c) ch[(a) + ido * ((b) + 2 * (c))]
+#define WA(x, i) wa[(i) + (x) * (ido - 1)]
+    for (int k = 0; k < l1; k++) PM(CH(0, 0, k), CH(ido - 1, 1, k), CC(0, k, 0), CC(0, k, 1));
+    if ((ido & 1) == 0)
+        for (int k = 0; k < l1; k++) {
+            CH(0, 1, k) = -CC(ido - 1, k, 1);
+            CH(ido - 1, 0, k) = CC(ido - 1, k, 0);
+        }
+    if (ido <= 2) return;
+    for (int k = 0; k < l1; k++)
+        for (int i = 2; i < ido; i += 2) {
+            int ic = ido - i;
+            float tr2, ti2;
+            MULPM(tr2, ti2, WA(0, i - 2), WA(0, i - 1), CC(i - 1, k, 1), CC(i, k, 1));
+            PM(CH(i - 1, 0, k), CH(ic - 1, 1, k), CC(i - 1, k, 0), tr2);
+            PM(CH(i, 0, k), CH(ic, 1, k), ti2, CC(i, k, 0));
+        }
+#undef CC
+#undef CH
+#undef WA
+}
+
+/* forward radix 4 */
+static void radf4(int ido, int l1, const float *cc, float *ch, const float *wa)
+{
+#define CC(a, b, c) cc[(a) + ido * ((b) + l1 * (c))]
+#define CH(a, b, c) ch[(a) + ido * ((b) + 4 * (c))]
+#define WA(x, i) wa[(i) + (x) * (ido - 1)]
+    for (int k = 0; k < l1; k++) {
+        float tr1, tr2;
+        PM(tr1, CH(0, 2, k), CC(0, k, 3), CC(0, k, 1));
+        PM(tr2, CH(ido - 1, 1, k), CC(0, k, 0), CC(0, k, 2));
+        PM(CH(0, 0, k), CH(ido - 1, 3, k), tr2, tr1);
+    }
+    if ((ido & 1) == 0)
+        for (int k = 0; k < l1; k++) {
+            float ti1 = -HSQT2F * (CC(ido - 1, k, 1) + CC(ido - 1, k, 3));
+            float tr1 = HSQT2F * (CC(ido - 1, k, 1) - CC(ido - 1, k, 3));
+            PM(CH(ido - 1, 0, k), CH(ido - 1, 2, k), CC(ido - 1, k, 0), tr1);
+            PM(CH(0, 3, k), CH(0, 1, k), ti1, CC(ido - 1, k, 2));
+        }
+    if (ido <= 2) return;
+    for (int k = 0; k < l1; k++)
+        for (int i = 2; i < ido; i += 2) {
+            int ic = ido - i;
+            float ci2, ci3, ci4, cr2, cr3, cr4, ti1, ti2, ti3, ti4, tr1, tr2, tr3, tr4;
+            MULPM(cr2, ci2, WA(0, i - 2), WA(0, i - 1), CC(i - 1, k, 1), CC(i, k, 1));
+            MULPM(cr3, ci3, WA(1, i - 2), WA(1, i - 1), CC(i - 1, k, 2), CC(i, k, 2));
+            MULPM(cr4, ci4, WA(2, i - 2), WA(2, i - 1), CC(i - 1, k, 3), CC(i, k, 3));
+            PM(tr1, tr4, cr4, cr2);
+            PM(ti1, ti4, ci2, ci4);
+            PM(tr2, tr3, CC(i - 1, k, 0), cr3);
+            PM(ti2, ti3, CC(i, k, 0), ci3);
+            PM(CH(i - 1, 0, k), CH(ic - 1, 3, k), tr2, tr1);
+            PM(CH(i, 0, k), CH(ic, 3, k), ti1, ti2);
+            PM(CH(i - 1, 2, k), CH(ic - 1, 1, k), tr3, ti4);
+            PM(CH(i, 2, k), CH(ic, 1, k), tr4, ti3);
+        }
+#undef CC
+#undef CH
+#undef WA
+}
+
+/* rfftp::exec with copy_and_norm(fct) */
+static void rfft_exec(const dct_plan *p, float *c, float fct, int r2hc)
+{
+    const int n = p->n, nf = p->nf;
+    float ch[ORC_MAXB];
+    float *p1 = c, *p2 = ch;
+    if (r2hc) {
+        for (int k1 = 0, l1 = n; k1 < nf; ++k1) {
+            int k = nf - k1 - 1, ip = p->fct[k], ido = n / l1;
+            l1 /= ip;
+            if (ip == 4) radf4(ido, l1, p1, p2, p->tw[k]);
+            else radf2(ido, l1, p1, p2, p->tw[k]);
+            float *t = p1; p1 = p2; p2 = t;
+        }
+    } else {
+        for (int k = 0, l1 = 1; k < nf; k++) {
+            int ip = p->fct[k], ido = n / (ip * l1);
+            if (ip == 4) radb4(ido, l1, p1, p2, p->tw[k]);
+            else radb2(ido, l1, p1, p2, p->tw[k]);
+            float *t = p1; p1 = p2; p2 = t;
+            l1 *= ip;
+        }
+    }
+    if (p1 != c) {
+        if (fct != 1.0f) for (int i = 0; i < n; ++i) c[i] = fct * p1[i];
+        else memcpy(c, p1, sizeof(float) * n);
+    } else if (fct != 1.0f) {
+        for (int i = 0; i < n; ++i) c[i] *= fct;
+    }
+}
+
+/* T_dcst23::exec, type 2 (forward DCT), cosine=true, ortho=true */
+static void dct2_1d(const dct_plan *p, float *c)
+{
+    const int N = p->n, NS2 = (N + 1) / 2;
+    c[0] *= 2.0f;
+    if ((N & 1) == 0) c[N - 1] *= 2.0f;
+    for (int k = 1; k < N - 1; k += 2) { float t = c[k + 1]; c[k + 1] = t - c[k]; c[k] = c[k] + t; }
+    rfft_exec(p, c, p->norm, 0);
+    for (int k = 1, kc = N - 1; k < NS2; ++k, --kc) {
+        float t1 = p->dtw[k - 1] * c[kc] + p->dtw[kc - 1] * c[k];
+        float t2 = p->dtw[k - 1] * c[k] - p->dtw[kc - 1] * c[kc];
+        c[k] = 0.5f * (t1 + t2);
+        c[kc] = 0.5f * (t1 - t2);
+    }
+    if ((N & 1) == 0) c[NS2] *= p->dtw[NS2 - 1];
+    c[0] *= SQRT2F * 0.5f;
+}
+
+/* T_dcst23::exec, type 3 (inverse DCT), cosine=true, ortho=true */
+static void dct3_1d(const dct_plan *p, float *c)
+{
+    const int N = p->n, NS2 = (N + 1) / 2;
+    c[0] *= SQRT2F;
+    for (int k = 1, kc = N - 1; k < NS2; ++k, --kc) {
+        float t1 = c[k] + c[kc], t2 = c[k] - c[kc];
+        c[k] = p->dtw[k - 1] * t2 + p->dtw[kc - 1] * t1;
+        c[kc] = p->dtw[k - 1] * t1 - p->dtw[kc - 1] * t2;
+    }
+    if ((N & 1) == 0) c[NS2] *= 2.0f * p->dtw[NS2 - 1];
+    rfft_exec(p, c, p->norm, 1);
+    for (int k = 1; k < N - 1; k += 2) { float t = c[k]; c[k] = t - c[k + 1]; c[k + 1] = t + c[k + 1]; }
+}
+
+/* watermarking.py:76-83: dct(dct(block.T).T) -- axis 0 (columns) first, then rows */
+static void dct2d(const dct_plan *p, float *blk, int inverse)
+{
+    const int n = p->n;
+    float col[ORC_MAXB];
+    for (int j = 0; j < n; ++j) {
+        for (int i = 0; i < n; ++i) col[i] = blk[i * n + j];
+        if (inverse) dct3_1d(p, col); else dct2_1d(p, col);
+        for (int i = 0; i < n; ++i) blk[i * n + j] = col[i];
+    }
+    for (int i = 0; i < n; ++i) {
+        if (inverse) dct3_1d(p, blk + i * n); else dct2_1d(p, blk + i * n);
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* N5 / N6: SVD of one b x b block -- specified one-sided Jacobi in f64     */
+/* ------------------------------------------------------------------------ */
+#define JAC_MAX_SWEEPS 32
+/* Rotate pair (i,j) iff   gamma^2 > TOL2 * alpha * beta          (relative, TOL = 2^-50)
+ *                   and   gamma^2 > C * (alpha + beta)           (noise floor, C = 2^-103 * F)
+ * with F = ||D||_F^2.  Rotations against large columns leave rounding noise of
+ * about eps*sigma_max in every column; the second test stops rotations that only
+ * chase that noise (gamma's noise is ~eps*sigma_max*(|a_i|+|a_j|), and
+ * (|a_i|+|a_j|)^2 <= 2(alpha+beta)).  Without it rank-deficient blocks never
+ * converge; with an F-proportional floor instead, tiny singular triplets stay
+ * unresolved and structured covers lose bit-exactness. */
+#define JAC_TOL2 7.888609052210118e-31 /* 2^-100 */
+#define JAC_C2 9.860761315262648e-32   /* 2^-103 = 2 * (2^-52)^2 */
+
+/* Number of contiguous row chunks whose fma-chain partial sums are combined by a
+ * balanced pairwise tree (matches the HIP layout: P lanes per block hold P row
+ * chunks).  DESIGN.md 3.4. */
+static int jac_chunks(int b) { return b == 16 ? 8 : b == 8 ? 2 : 1; }
+
+static double tree_sum(double *v, int n)
+{
+    while (n > 1) {
+        for (int k = 0; k < n / 2; ++k) v[k] = v[2 * k] + v[2 * k + 1];
+        n /= 2;
+    }
+    return v[0];
+}
+
+/* sum_r x[r*ldx] * y[r*ldy] in the contract order */
+static double cdot(const double *x, const double *y, int ld, int b)
+{
+    const int P = jac_chunks(b), R = b / P;
+    double part[ORC_MAXB];
+    for (int q = 0; q < P; ++q) {
+        double acc = 0.0;
+        for (int r = q * R; r < (q + 1) * R; ++r) acc = fma(x[r * ld], y[r * ld], acc);
+        part[q] = acc;
+    }
+    return tree_sum(part, P);
+}
+
+/* round-robin (circle method) pair schedule: round s, slot p -> (i, j), i < j */
+static void jac_pairs(int b, int s, int p, int *pi, int *pj)
+{
+    /* L = [0, 1..b-1 rotated by s]; pairs (L[p], L[b-1-p]) */
+    int L[ORC_MAXB];
+    L[0] = 0;
+    for (int k = 1; k < b; ++k) L[k] = 1 + ((k - 1 + s) % (b - 1));
+    int a = L[p], c = L[b - 1 - p];
+    *pi = a < c ? a : c;
+    *pj = a < c ? c : a;
+}
+
+/* A (b x b, row-major, f64) is overwritten with A*V; V (row-major) accumulates.  Returns sweeps done. */
+static int jacobi(double *A, double *V, int b, int want_v)
+{
+    int sweep;
+    double F = 0.0;
+    for (int k = 0; k < b; ++k) F += cdot(A + k, A + k, b, b);
+    const double c2 = JAC_C2 * F;
+    for (sweep = 0; sweep < JAC_MAX_SWEEPS; ++sweep) {
+        int rotated = 0;
+        for (int s = 0; s < b - 1; ++s) {
+            for (int p = 0; p < b / 2; ++p) {
+                int i, j;
+                jac_pairs(b, s, p, &i, &j);
+                const double alpha = cdot(A + i, A + i, b, b);
+                const double beta = cdot(A + j, A + j, b, b);
+                const double gamma = cdot(A + i, A + j, b, b);
+                const double g2 = gamma * gamma;
+                if (g2 <= c2 * (alpha + beta) || g2 <= (JAC_TOL2 * alpha) * beta) continue;
+                rotated = 1;
+                const double zeta = (beta - alpha) / (2.0 * gamma);
+                const double t = copysign(1.0, zeta) / (fabs(zeta) + sqrt(fma(zeta, zeta, 1.0)));
+                const double c = 1.0 / sqrt(fma(t, t, 1.0));
+                const double sn = c * t;
+                for (int r = 0; r < b; ++r) {
+                    const double x = A[r * b + i], y = A[r * b + j];
+                    A[r * b + i] = fma(-sn, y, c * x);
+                    A[r * b + j] = fma(sn, x, c * y);
+                }
+                if (want_v)
+                    for (int r = 0; r < b; ++r) {
+                        const double x = V[r * b + i], y = V[r * b + j];
+                        V[r * b + i] = fma(-sn, y, c * x);
+                        V[r * b + j] = fma(sn, x, c * y);
+                    }
+            }
+        }
+        if (!rotated) { ++sweep; break; }
+    }
+    return sweep;
+}
+
+
+
+/* Full SVD of one block: D (b x b f32 row-major) -> U (b x b), S (b), Vt (b x b), f32, sorted descending.
+ * Returns number of sweeps. */
+int orc_svd_block(const float *D, int b, float *U, float *S, float *Vt)
+{
+    double A[ORC_MAXB * ORC_MAXB], V[ORC_MAXB * ORC_MAXB], sig[ORC_MAXB];
+    int allzero = 1;
+    for (int k = 0; k < b * b; ++k) { A[k] = D[k]; if (D[k] != 0.0f) allzero = 0; }
+    for (int r = 0; r < b; ++r) for (int k = 0; k < b; ++k) V[r * b + k] = (r == k) ? 1.0 : 0.0;
+    if (allzero) {
+        /* N6: LAPACK returns U = I, Vt = I for the zero matrix */
+        for (int r = 0; r < b; ++r) for (int k = 0; k < b; ++k) { U[r * b + k] = (r == k); Vt[r * b + k] = (r == k); }
+        for (int k = 0; k < b; ++k) S[k] = 0.0f;
+        return 0;
+    }
+    int sweeps = jacobi(A, V, b, 1);
+    float Uf[ORC_MAXB * ORC_MAXB], Vf[ORC_MAXB * ORC_MAXB];
+    for (int k = 0; k < b; ++k) {
+        sig[k] = sqrt(cdot(A + k, A + k, b, b));
+        if (sig[k] == 0.0) {
+            for (int r = 0; r < b; ++r) Uf[r * b + k] = 0.0f;
+        } else {
+            const double inv = 1.0 / sig[k];
+            for (int r = 0; r < b; ++r) Uf[r * b + k] = (float)(A[r * b + k] * inv);
+        }
+        for (int r = 0; r < b; ++r) Vf[r * b + k] = (float)V[r * b + k];
+    }
+    /* odd-even transposition sort, descending on the f64 singular values */
+    for (int round = 0; round < b; ++round)
+        for (int k = round & 1; k + 1 < b; k += 2)
+            if (sig[k] < sig[k + 1]) {
+                double ts = sig[k]; sig[k] = sig[k + 1]; sig[k + 1] = ts;
+                for (int r = 0; r < b; ++r) {
+                    float tu = Uf[r * b + k]; Uf[r * b + k] = Uf[r * b + k + 1]; Uf[r * b + k + 1] = tu;
+                    float tv = Vf[r * b + k]; Vf[r * b + k] = Vf[r * b + k + 1]; Vf[r * b + k + 1] = tv;
+                }
+            }
+    for (int k = 0; k < b; ++k) {
+        S[k] = (float)sig[k];
+        for (int r = 0; r < b; ++r) { U[r * b + k] = Uf[r * b + k]; Vt[k * b + r] = Vf[r * b + k]; }
+    }
+    return sweeps;
+}
+
+/* sigma_1 only (extract path): f32(max_k ||(A V)_k||) */
+float orc_sigma1_block(const float *D, int b)
+{
+    double A[ORC_MAXB * ORC_MAXB];
+    for (int k = 0; k < b * b; ++k) A[k] = D[k];
+    jacobi(A, NULL, b, 0);
+    double m = 0.0;
+    for (int k = 0; k < b; ++k) {
+        double s = sqrt(cdot(A + k, A + k, b, b));
+        if (s > m) m = s;
+    }
+    return (float)m;
+}
+
+/* N7 blend + N8 reconstruct: S'[0] = f32(f64(S0) + alpha*(w/255.0)); M = U @ (diag(S') @ Vt) */
+void orc_blend_reconstruct(const float *U, const float *S, const float *Vt, int b, uint8_t w, double alpha, float *M)
+{
+    float Sp[ORC_MAXB], B[ORC_MAXB * ORC_MAXB];
+    for (int k = 0; k < b; ++k) Sp[k] = S[k];
+    Sp[0] = (float)((double)S[0] + alpha * ((double)w / 255.0));
+    for (int k = 0; k < b; ++k) for (int j = 0; j < b; ++j) B[k * b + j] = Sp[k] * Vt[k * b + j];
+    for (int i = 0; i < b; ++i)
+        for (int j = 0; j < b; ++j) {
+            float acc = 0.0f;
+            for (int k = 0; k < b; ++k) acc = fmaf(U[i * b + k], B[k * b + j], acc);
+            M[i * b + j] = acc;
+        }
+}
+
+/* ------------------------------------------------------------------------ */
+/* Exported stage functions                                                 */
+/* ------------------------------------------------------------------------ */
+int orc_supported_block(int b) { return b == 4 || b == 8 || b == 16; }
+
+void orc_rgb_to_ycbcr(const uint8_t *rgb, int64_t npix, float *ycc)
+{
+    for (int64_t p = 0; p < npix; ++p) colour_fwd(rgb[3 * p], rgb[3 * p + 1], rgb[3 * p + 2], ycc + 3 * p, ycc + 3 * p + 1, ycc + 3 * p + 2);
+}
+
+void orc_ycbcr_to_rgb(const float *ycc, int64_t npix, uint8_t *rgb)
+{
+    for (int64_t p = 0; p < npix; ++p) colour_inv(ycc[3 * p], ycc[3 * p + 1], ycc[3 * p + 2], rgb + 3 * p);
+}
+
+/* nb blocks of b x b, row-major each, in place */
+void orc_dct2d_blocks(float *blocks, int64_t nb, int b, int inverse)
+{
+    const dct_plan *p = plan_for(b);
+    for (int64_t k = 0; k < nb; ++k) dct2d(p, blocks + k * b * b, inverse);
+}
+
+/* 1-D transforms along contiguous rows (for pinning against scipy row-wise) */
+void orc_dct_rows(float *x, int64_t nrows, int n, int inverse)
+{
+    const dct_plan *p = plan_for(n);
+    for (int64_t k = 0; k < nrows; ++k) { if (inverse) dct3_1d(p, x + k * n); else dct2_1d(p, x + k * n); }
+}
+
+int orc_svd_blocks(const float *D, int64_t nb, int b, float *U, float *S, float *Vt, int32_t *sweeps)
+{
+    int maxs = 0;
+    for (int64_t k = 0; k < nb; ++k) {
+        int s = orc_svd_block(D + k * b * b, b, U + k * b * b, S + k * b, Vt + k * b * b);
+        if (sweeps) sweeps[k] = s;
+        if (s > maxs) maxs = s;
+    }
+    return maxs;
+}
+
+/* Y plane (H x W f32) -> DCT blocks (nbh*nbw, b, b) */
+void orc_gather_blocks(const float *Y, int H, int W, int b, float *blocks)
+{
+    const int nbh = H / b, nbw = W / b;
+    for (int bi = 0; bi < nbh; ++bi)
+        for (int bj = 0; bj < nbw; ++bj) {
+            float *blk = blocks + ((int64_t)bi * nbw + bj) * b * b;
+            for (int r = 0; r < b; ++r)
+                for (int c = 0; c < b; ++c) blk[r * b + c] = Y[(int64_t)(bi * b + r) * W + bj * b + c];
+        }
+}
+
+void orc_scatter_blocks(const float *blocks, int H, int W, int b, float *Y)
+{
+    const int nbh = H / b, nbw = W / b;
+    for (int bi = 0; bi < nbh; ++bi)
+        for (int bj = 0; bj < nbw; ++bj) {
+            const float *blk = blocks + ((int64_t)bi * nbw + bj) * b * b;
+            for (int r = 0; r < b; ++r)
+                for (int c = 0; c < b; ++c) Y[(int64_t)(bi * b + r) * W + bj * b + c] = blk[r * b + c];
+        }
+}
+
+/* One block row (bi) of the embed: Y plane updated in place. */
+static void embed_block_row(float *Y, int W, int b, int bi, int nbw, const uint8_t *wm, double alpha)
+{
+    const dct_plan *p = plan_for(b);
+    float D[ORC_MAXB * ORC_MAXB], U[ORC_MAXB * ORC_MAXB], Vt[ORC_MAXB * ORC_MAXB], S[ORC_MAXB], M[ORC_MAXB * ORC_MAXB];
+    for (int bj = 0; bj < nbw; ++bj) {
+        for (int r = 0; r < b; ++r)
+            for (int c = 0; c < b; ++c) D[r * b + c] = Y[(int64_t)(bi * b + r) * W + bj * b + c];
+        dct2d(p, D, 0);                                    /* :192 */
+        orc_svd_block(D, b, U, S, Vt);                     /* :195 */
+        orc_blend_reconstruct(U, S, Vt, b, wm[(int64_t)bi * nbw + bj], alpha, M); /* :198-201 */
+        dct2d(p, M, 1);                                    /* :204 */
+        for (int r = 0; r < b; ++r)
+            for (int c = 0; c < b; ++c) Y[(int64_t)(bi * b + r) * W + bj * b + c] = M[r * b + c]; /* :207-210 */
+    }
+}
+
+static int clamp_threads(int nthreads) { return nthreads < 1 ? 1 : nthreads; }
+
+/* embed_watermark arithmetic for one frame (watermarking.py:163-216).
+ * rgb: H x W x 3 u8; wm: (H/b) x (W/b) u8 tile (already resized); out: H x W x 3 u8. */
+int orc_embed_frame(const uint8_t *rgb, int H, int W, const uint8_t *wm, int b, double alpha, uint8_t *out, int nthreads)
+{
+    if (!orc_supported_block(b) || H < 0 || W < 0) return -1;
+    plans_init();
+    const int64_t npix = (int64_t)H * W;
+    float *ycc = (float *)malloc(sizeof(float) * 3 * (npix ? npix : 1));
+    float *Y = (float *)malloc(sizeof(float) * (npix ? npix : 1));
+    if (!ycc || !Y) { free(ycc); free(Y); return -2; }
+    nthreads = clamp_threads(nthreads);
+#pragma omp parallel for num_threads(nthreads) schedule(static)
+    for (int64_t q = 0; q < npix; ++q) {
+        colour_fwd(rgb[3 * q], rgb[3 * q + 1], rgb[3 * q + 2], ycc + 3 * q, ycc + 3 * q + 1, ycc + 3 * q + 2);
+        Y[q] = ycc[3 * q];
+    }
+    const int nbh = H / b, nbw = W / b;
+#pragma omp parallel for num_threads(nthreads) schedule(dynamic, 1)
+    for (int bi = 0; bi < nbh; ++bi) embed_block_row(Y, W, b, bi, nbw, wm, alpha);
+#pragma omp parallel for num_threads(nthreads) schedule(static)
+    for (int64_t q = 0; q < npix; ++q) colour_inv(Y[q], ycc[3 * q + 1], ycc[3 * q + 2], out + 3 * q);
+    free(ycc);
+    free(Y);
+    return 0;
+}
+
+/* extract_watermark arithmetic for one frame pair (watermarking.py:241-289).
+ * Both images H x W x 3 (the original already cropped to the watermarked size). out: (H/b) x (W/b). */
+int orc_extract_frame(const uint8_t *wrgb, const uint8_t *orgb, int H, int W, int b, double alpha, uint8_t *out, int nthreads)
+{
+    if (!orc_supported_block(b) || H < 0 || W < 0) return -1;
+    plans_init();
+    const int nbh = H / b, nbw = W / b;
+    const float alpha32 = (float)alpha;
+    const dct_plan *p = plan_for(b);
+    nthreads = clamp_threads(nthreads);
+#pragma omp parallel for num_threads(nthreads) schedule(dynamic, 1)
+    for (int bi = 0; bi < nbh; ++bi) {
+        float Dw[ORC_MAXB * ORC_MAXB], Do[ORC_MAXB * ORC_MAXB];
+        for (int bj = 0; bj < nbw; ++bj) {
+            for (int r = 0; r < b; ++r)
+                for (int c = 0; c < b; ++c) {
+                    const int64_t q = (int64_t)(bi * b + r) * W + bj * b + c;
+                    float y, cb, cr;
+                    colour_fwd(wrgb[3 * q], wrgb[3 * q + 1], wrgb[3 * q + 2], &y, &cb, &cr);
+                    Dw[r * b + c] = y;
+                    colour_fwd(orgb[3 * q], orgb[3 * q + 1], orgb[3 * q + 2], &y, &cb, &cr);
+                    Do[r * b + c] = y;
+                }
+            dct2d(p, Dw, 0);
+            dct2d(p, Do, 0);
+            const float sw = orc_sigma1_block(Dw, b), so = orc_sigma1_block(Do, b);
+            /* :285 numpy-2 NEP 50: float32 - float32, then / python float in float32 */
+            const float e = (sw - so) / alpha32;
+            /* :288-289 stored in f64, clip [0,1], *255 (f64), astype(uint8) */
+            double d = (double)e;
+            if (d < 0.0) d = 0.0;
+            if (d > 1.0) d = 1.0;
+            out[(int64_t)bi * nbw + bj] = (uint8_t)(d * 255.0);
+        }
+    }
+    return 0;
+}
+
+/* Batched helpers for the CPU baseline (frames laid out back to back). */
+int orc_embed_batch(const uint8_t *rgb, int64_t n, int H, int W, const uint8_t *wm, int b, double alpha, uint8_t *out, int nthreads)
+{
+    const int64_t fs = (int64_t)H * W * 3;
+    for (int64_t f = 0; f < n; ++f) {
+        int rc = orc_embed_frame(rgb + f * fs, H, W, wm, b, alpha, out + f * fs, nthreads);
+        if (rc) return rc;
+    }
+    return 0;
+}
+
+int orc_extract_batch(const uint8_t *wrgb, const uint8_t *orgb, int64_t n, int H, int W, int b, double alpha, uint8_t *out, int nthreads)
+{
+    const int64_t fs = (int64_t)H * W * 3, ts = (int64_t)(H / b) * (W / b);
+    for (int64_t f = 0; f < n; ++f) {
+        int rc = orc_extract_frame(wrgb + f * fs, orgb + f * fs, H, W, b, alpha, out + f * ts, nthreads);
+        if (rc) return rc;
+    }
+    return 0;
+}
+
+/* Synthetic input generator shared with the GPU generator:
+ * byte = splitmix64(seed ^ (frame << 40) ^ idx) & 0xFF over the linear HWC index. */
+static inline uint64_t splitmix64(uint64_t x)
+{
+    x += 0x9E3779B97F4A7C15ULL;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
+    return x ^ (x >> 31);
+}
+
+void orc_synth_bytes(uint64_t seed, int64_t frame0, int64_t nframes, int64_t frame_bytes, uint8_t *out)
+{
+    for (int64_t f = 0; f < nframes; ++f)
+        for (int64_t i = 0; i < frame_bytes; ++i)
+            out[f * frame_bytes + i] = (uint8_t)(splitmix64(seed ^ ((uint64_t)(frame0 + f) << 40) ^ (uint64_t)i) & 0xFF);
+}
