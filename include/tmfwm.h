@@ -1,0 +1,105 @@
+/*
+ * tmfwm.h -- C ABI of libtmfwm.so, the MI355X (gfx950) implementation of the
+ * block-wise DCT+SVD watermark path of ThatsMyFace (modules/watermarking.py).
+ *
+ * Drop-in boundary: the reference's Python functions keep their signatures
+ * (thatsmyface_amd/watermarking.py mirrors them); underneath, each per-pixel /
+ * per-block loop of the reference becomes one call below.  Plain pointers and
+ * sizes only.  The caller owns every buffer.  No exceptions cross the ABI.
+ *
+ * Status codes: 0 ok, negative errno-style values on error; the thread-local
+ * message is available from tmfwm_last_error().  All entry points are
+ * re-entrant (Streamlit runs sessions on threads): no mutable global state,
+ * per-call or per-thread HIP streams.
+ *
+ * Memory: mem_kind = TMFWM_MEM_DEVICE -> every pointer is device memory of the
+ * current HIP device (e.g. a torch tensor's data_ptr()); work is enqueued on
+ * `hip_stream` (NULL = the per-thread default stream) and the call returns
+ * without synchronising.  mem_kind = TMFWM_MEM_HOST -> pointers are host
+ * memory; the library stages through device memory and returns after the
+ * results are back in host memory.
+ *
+ * Image layout: n_frames frames of height x width x 3 uint8, HWC interleaved
+ * (numpy / PIL "RGB" order), frame i at base + i * frame_stride bytes
+ * (frame_stride >= height*width*3).  Block grid: nbh = height / block,
+ * nbw = width / block.  Supported block sizes: 4, 8, 16 (others return
+ * TMFWM_ERR_UNSUPPORTED).
+ */
+#ifndef TMFWM_H
+#define TMFWM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TMFWM_ABI_VERSION 1
+
+#define TMFWM_MEM_HOST 0
+#define TMFWM_MEM_DEVICE 1
+
+#define TMFWM_OK 0
+#define TMFWM_ERR_INVALID (-22)     /* bad argument (EINVAL) */
+#define TMFWM_ERR_NOMEM (-12)       /* device allocation failed (ENOMEM) */
+#define TMFWM_ERR_HIP (-5)          /* HIP runtime / launch error (EIO) */
+#define TMFWM_ERR_UNSUPPORTED (-95) /* block size not 4/8/16 (EOPNOTSUPP) */
+#define TMFWM_ERR_NODEVICE (-19)    /* no usable gfx950 device (ENODEV) */
+
+/* ABI version (TMFWM_ABI_VERSION) compiled into the library. */
+int tmfwm_abi_version(void);
+
+/* Message of the last failed call on this thread ("" if none). */
+const char *tmfwm_last_error(void);
+
+/* Number of visible HIP devices (0 when none); never fails. */
+int tmfwm_device_count(void);
+
+/*
+ * Embed: replaces the body of embed_watermark() (watermarking.py:163-219):
+ * RGB->YCbCr (:166), per-block 2-D DCT (:192), SVD (:195), S[0] += alpha*w/255
+ * (:198), U diag(S) Vt (:201), IDCT (:204), write-back (:207-213), YCbCr->RGB
+ * (:216).  wm_tile is the already-resized watermark (resize_watermark :86,
+ * host side), nbh x nbw uint8, shared by all frames.  out may not alias rgb.
+ */
+int tmfwm_embed(const uint8_t *rgb, int64_t n_frames, int32_t height, int32_t width, int64_t frame_stride,
+                const uint8_t *wm_tile, int32_t block, double alpha, uint8_t *out, int32_t mem_kind, void *hip_stream);
+
+/*
+ * Extract: replaces the body of extract_watermark() (watermarking.py:246-292):
+ * luma of both images, per-block sigma_1 of the DCT of each, (s_w - s_o)/alpha
+ * in float32, clip to [0,1], *255, truncation.  Both images have the same
+ * height x width (the caller crops a larger original, as the reference's
+ * slicing does).  out_tiles: n_frames tiles of nbh x nbw uint8, back to back.
+ */
+int tmfwm_extract(const uint8_t *wm_rgb, const uint8_t *orig_rgb, int64_t n_frames, int32_t height, int32_t width,
+                  int64_t frame_stride, int32_t block, double alpha, uint8_t *out_tiles, int32_t mem_kind,
+                  void *hip_stream);
+
+/* rgb_to_ycbcr (watermarking.py:23): npix RGB uint8 pixels -> npix x 3 float32 (Y, Cb+0.5, Cr+0.5). */
+int tmfwm_rgb_to_ycbcr(const uint8_t *rgb, int64_t npix, float *ycc, int32_t mem_kind, void *hip_stream);
+
+/* ycbcr_to_rgb (watermarking.py:53): npix x 3 float32 -> RGB uint8 (clip, *255, truncate). */
+int tmfwm_ycbcr_to_rgb(const float *ycc, int64_t npix, uint8_t *rgb, int32_t mem_kind, void *hip_stream);
+
+/* apply_dct_to_block / apply_idct_to_block (watermarking.py:76, :81) on n_blocks
+ * contiguous row-major block x block float32 blocks, in place. */
+int tmfwm_dct2d_blocks(float *blocks, int64_t n_blocks, int32_t block, int32_t inverse, int32_t mem_kind,
+                       void *hip_stream);
+
+/* np.linalg.svd(D) as the reference consumes it (watermarking.py:195): U, S
+ * (descending), Vt in float32 for n_blocks blocks.  sweeps (optional, may be
+ * NULL) receives the Jacobi sweeps executed per block. */
+int tmfwm_svd_blocks(const float *D, int64_t n_blocks, int32_t block, float *U, float *S, float *Vt, int32_t *sweeps,
+                     int32_t mem_kind, void *hip_stream);
+
+/* Synthetic frames generated in device memory (bench inputs):
+ * out[f*frame_bytes + i] = splitmix64(seed ^ ((frame0+f) << 40) ^ i) & 0xFF. */
+int tmfwm_synth_frames(uint64_t seed, int64_t frame0, int64_t n_frames, int64_t frame_bytes, uint8_t *out,
+                       void *hip_stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* TMFWM_H */

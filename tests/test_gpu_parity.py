@@ -1,0 +1,249 @@
+"""GPU parity: libtmfwm.so's HIP kernels vs the oracle (oracle/tmfwm_oracle.c) and the
+reference's golden fixtures.  Bar: bit-exact bytes, 0-ULP DCT coefficients, and
+bit-identical U/S/Vt from the Jacobi SVD.  Runs on the MI355X box (-m gpu).
+"""
+import hashlib
+
+import numpy as np
+import pytest
+from PIL import Image
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need a ROCm device"
+    from thatsmyface_amd import _lib
+
+    assert _lib.device_count() > 0
+    return torch.device("cuda", 0)
+
+
+def _u8(seed, shape):
+    return np.random.default_rng(seed).integers(0, 256, shape, dtype=np.uint8)
+
+
+def _blocks_of(Y, b):
+    H, W = Y.shape
+    nbh, nbw = H // b, W // b
+    return np.ascontiguousarray(Y[: nbh * b, : nbw * b].reshape(nbh, b, nbw, b).transpose(0, 2, 1, 3).reshape(-1, b, b))
+
+
+# ---------------------------------------------------------------- stages
+def test_colour_tables_exhaustive_gpu(dev, golden):
+    from thatsmyface_amd import watermarking as W
+
+    _, meta = golden
+    c = np.arange(1 << 24, dtype=np.uint32)
+    rgb = np.stack([(c >> 16) & 255, (c >> 8) & 255, c & 255], -1).astype(np.uint8).reshape(4096, 4096, 3)
+    ycc = W.rgb_to_ycbcr(rgb)
+    assert sha(ycc) == meta["kats"]["colour_fwd_table_sha256"]
+    assert sha(W.ycbcr_to_rgb(ycc)) == meta["kats"]["colour_roundtrip_table_sha256"]
+
+
+@pytest.mark.parametrize("b", [4, 8, 16])
+def test_dct_blocks_gpu(dev, b):
+    from thatsmyface_amd import watermarking as W
+
+    rng = np.random.default_rng(b)
+    x = np.concatenate([rng.random((4000, b, b), dtype=np.float32),
+                        (rng.standard_normal((1000, b, b)) * 1e-3).astype(np.float32)])
+    d = W.apply_dct_to_block(x)
+    assert np.array_equal(d.view(np.uint32), O.dct2d_blocks(x).view(np.uint32))
+    i = W.apply_idct_to_block(x)
+    assert np.array_equal(i.view(np.uint32), O.dct2d_blocks(x, inverse=True).view(np.uint32))
+
+
+def _svd_corpus(b):
+    from golden.gen_golden import cover
+
+    out = []
+    for kind, seed in (("noise", 1), ("smooth", 2), ("qr", 3), ("blocky", 4), ("diagonal", 5), ("flat", 6), ("black", 7)):
+        Y = O.rgb_to_ycbcr(cover(kind, 128, 128, seed))[..., 0]
+        out.append(O.dct2d_blocks(_blocks_of(Y, b)))
+    return np.concatenate(out)
+
+
+@pytest.mark.parametrize("b", [4, 8, 16])
+def test_svd_blocks_gpu_bit_identical(dev, b):
+    from thatsmyface_amd import batch
+
+    D = _svd_corpus(b)
+    U, S, Vt, sw = batch.svd_blocks(torch.from_numpy(D).to(dev))
+    Uo, So, Vo, swo = O.svd_blocks(D)
+    assert np.array_equal(S.cpu().numpy().view(np.uint32), So.view(np.uint32))
+    assert np.array_equal(U.cpu().numpy().view(np.uint32), Uo.view(np.uint32))
+    assert np.array_equal(Vt.cpu().numpy().view(np.uint32), Vo.view(np.uint32))
+    # the wave runs until its slowest block converges; never fewer sweeps than the oracle
+    assert (sw.cpu().numpy() >= swo).all()
+
+
+# ---------------------------------------------------------------- drop-in API on the golden fixtures
+def _cover_image(arr):
+    if arr.ndim == 2:
+        return Image.fromarray(arr, "L")
+    if arr.shape[-1] == 4:
+        return Image.fromarray(arr, "RGBA")
+    return Image.fromarray(arr, "RGB")
+
+
+def test_golden_cases_dropin_gpu(dev, golden):
+    from test_oracle_golden import ILL_CONDITIONED
+
+    from thatsmyface_amd import watermarking as W
+
+    cases, meta = golden
+    for name, m in meta["cases"].items():
+        cov = _cover_image(cases[f"{name}/cover"])
+        wm = Image.fromarray(cases[f"{name}/wm"], "L")
+        settings = {"block_size": m["block"], "alpha": m["alpha"]}
+        emb = W.embed_watermark(cov, wm, m["preserve_ratio"], settings)
+        e = np.asarray(emb)
+        assert emb.mode == "RGB" and e.shape == cases[f"{name}/embed"].shape
+        assert np.array_equal(np.asarray(W.resize_watermark(wm, e.shape[0] // m["block"], e.shape[1] // m["block"],
+                                                            m["preserve_ratio"])), cases[f"{name}/tile"]), name
+        rgb = np.asarray(cov.convert("RGB"))
+        assert np.array_equal(e, O.embed_frame(rgb, cases[f"{name}/tile"], m["block"], m["alpha"])), name
+        if name not in ILL_CONDITIONED:
+            assert np.array_equal(e, cases[f"{name}/embed"]), name
+        ex = W.extract_watermark(Image.fromarray(cases[f"{name}/embed"]), cov, settings)
+        assert ex.mode == "L"
+        assert np.array_equal(np.asarray(ex), cases[f"{name}/extract"]), name
+
+
+def test_golden_png_bytes_watermark_gpu(dev, golden):
+    """watermark_data as PNG bytes (the app's call site, embed_watermark_page.py:529-531)."""
+    import io
+
+    from thatsmyface_amd import watermarking as W
+
+    cases, meta = golden
+    name = "noise_128x96_pr"
+    m = meta["cases"][name]
+    buf = io.BytesIO()
+    Image.fromarray(cases[f"{name}/wm"], "L").save(buf, format="PNG")
+    emb = W.embed_watermark(Image.fromarray(cases[f"{name}/cover"]), buf.getvalue(), True,
+                            {"block_size": m["block"], "alpha": m["alpha"]})
+    assert np.array_equal(np.asarray(emb), cases[f"{name}/embed"])
+
+
+def test_stages_gpu(dev, stages):
+    from thatsmyface_amd import watermarking as W
+
+    ycc = W.rgb_to_ycbcr(stages["cover"])
+    assert np.array_equal(ycc.view(np.uint32), stages["ycc"].view(np.uint32))
+    D = W.apply_dct_to_block(_blocks_of(np.ascontiguousarray(ycc[..., 0]), int(stages["block"])))
+    assert np.array_equal(D.view(np.uint32), stages["D"].view(np.uint32))
+    Yb = W.apply_idct_to_block(stages["M"])
+    assert np.array_equal(Yb.view(np.uint32), stages["Yblocks"].view(np.uint32))
+
+
+# ---------------------------------------------------------------- batches in HBM vs the oracle
+@pytest.mark.parametrize("b,h,w,n", [(8, 1080, 1920, 2), (8, 250, 333, 3), (16, 1088, 1920, 1), (4, 131, 258, 2),
+                                     (16, 200, 170, 2), (8, 2160, 3840, 1)])
+def test_batch_embed_extract_vs_oracle(dev, b, h, w, n):
+    from thatsmyface_amd import batch
+
+    frames = batch.synth_frames(n, h, w, seed=0xC0FFEE + b, device=dev)
+    tile = batch.synth_tile(h // b, w // b, device=dev)
+    host = frames.cpu().numpy()
+    assert np.array_equal(host.reshape(-1), O.synth_bytes(0xC0FFEE + b, 0, n, h * w * 3))
+    out = batch.embed_batch(frames, tile, b, 0.1)
+    ext = batch.extract_batch(out, frames, b, 0.1)
+    torch.cuda.synchronize()
+    t = tile.cpu().numpy()
+    for f in range(n):
+        ref = O.embed_frame(host[f], t, b, 0.1)
+        assert np.array_equal(out[f].cpu().numpy(), ref), (b, h, w, f)
+        assert np.array_equal(ext[f].cpu().numpy(), O.extract_frame(ref, host[f], b, 0.1)), (b, h, w, f)
+
+
+def test_batch_structured_covers_vs_oracle(dev):
+    """QR-like / black / flat covers: zero blocks (N6), rank-deficient and tied blocks."""
+    from golden.gen_golden import cover, wmark
+
+    from thatsmyface_amd import batch
+
+    for b in (4, 8, 16):
+        for kind in ("qr", "black", "flat", "smooth", "blocky", "diagonal"):
+            c = np.ascontiguousarray(cover(kind, 256, 320, 11))
+            t = wmark("qr", 256 // b, 320 // b, 12)
+            out = batch.embed_batch(torch.from_numpy(c[None]).to(dev), torch.from_numpy(t).to(dev), b, 0.15)
+            ref = O.embed_frame(c, t, b, 0.15)
+            assert np.array_equal(out[0].cpu().numpy(), ref), (b, kind)
+            ext = batch.extract_batch(out, torch.from_numpy(c[None]).to(dev), b, 0.15)
+            assert np.array_equal(ext[0].cpu().numpy(), O.extract_frame(ref, c, b, 0.15)), (b, kind)
+
+
+def test_unaligned_strided_frames(dev):
+    """Frames at odd byte offsets / strides take the byte-granular load path."""
+    from thatsmyface_amd import _lib
+
+    h, w, b = 64, 72, 8
+    raw = _u8(5, (3 * h * w * 3 + 7,))
+    stride = h * w * 3 + 1
+    src = torch.from_numpy(raw).to(dev)
+    tile = torch.from_numpy(_u8(6, (h // b, w // b))).to(dev)
+    out = torch.zeros_like(src)
+    L = _lib.load()
+    base = src.data_ptr() + 1
+    _lib.check(L.tmfwm_embed(base, 2, h, w, stride, tile.data_ptr(), b, 0.1, out.data_ptr() + 1, _lib.MEM_DEVICE,
+                             torch.cuda.current_stream().cuda_stream), "embed")
+    torch.cuda.synchronize()
+    o = out.cpu().numpy()
+    for f in range(2):
+        fr = raw[1 + f * stride: 1 + f * stride + h * w * 3].reshape(h, w, 3)
+        ref = O.embed_frame(fr, tile.cpu().numpy(), b, 0.1)
+        assert np.array_equal(o[1 + f * stride: 1 + f * stride + h * w * 3].reshape(h, w, 3), ref)
+
+
+def test_determinism_and_roundtrip_4k(dev):
+    """Full-size 4K batch: bit-identical reruns; extraction of every frame equals the
+    oracle's on a sampled frame; PSNR(watermarked, cover) in the reference's band."""
+    from thatsmyface_amd import batch
+
+    n, h, w, b = 4, 2160, 3840, 8
+    frames = batch.synth_frames(n, h, w, device=dev)
+    tile = batch.synth_tile(h // b, w // b, device=dev)
+    a = batch.embed_batch(frames, tile, b, 0.1)
+    a2 = batch.embed_batch(frames, tile, b, 0.1)
+    assert torch.equal(a, a2)
+    ex = batch.extract_batch(a, frames, b, 0.1)
+    f = 3
+    host = frames[f].cpu().numpy()
+    ref = O.embed_frame(host, tile.cpu().numpy(), b, 0.1)
+    assert np.array_equal(a[f].cpu().numpy(), ref)
+    assert np.array_equal(ex[f].cpu().numpy(), O.extract_frame(ref, host, b, 0.1))
+    mse = ((a.float() - frames.float()) ** 2).mean().item()
+    psnr = 10 * np.log10(255.0 ** 2 / mse)
+    assert 40.0 < psnr < 50.0, psnr  # 44.95 dB at alpha 0.1 on noise covers
+
+
+def test_empty_and_degenerate(dev):
+    from thatsmyface_amd import _lib, batch
+
+    # zero frames: no-op
+    z = torch.empty((0, 16, 16, 3), dtype=torch.uint8, device=dev)
+    batch.embed_batch(z, torch.zeros((2, 2), dtype=torch.uint8, device=dev), 8, 0.1)
+    # image smaller than a block: colour round trip only
+    small = torch.from_numpy(_u8(9, (1, 5, 7, 3))).to(dev)
+    out = batch.embed_batch(small, torch.zeros((0, 0), dtype=torch.uint8, device=dev), 8, 0.1)
+    ref = O.ycbcr_to_rgb(O.rgb_to_ycbcr(small[0].cpu().numpy()))
+    assert np.array_equal(out[0].cpu().numpy(), ref)
+    # host pointer passed as device memory is refused, not dereferenced
+    h = np.zeros((8, 8, 3), np.uint8)
+    with pytest.raises(ValueError):
+        _lib.check(_lib.load().tmfwm_embed(h.ctypes.data, 1, 8, 8, 192, h.ctypes.data, 8, 0.1, h.ctypes.data,
+                                           _lib.MEM_DEVICE, None), "embed")
+    with pytest.raises(NotImplementedError):
+        batch.embed_batch(torch.zeros((1, 12, 12, 3), dtype=torch.uint8, device=dev),
+                          torch.zeros((2, 2), dtype=torch.uint8, device=dev), 6, 0.1)

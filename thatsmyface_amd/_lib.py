@@ -1,0 +1,95 @@
+"""ctypes binding of libtmfwm.so (C ABI declared in include/tmfwm.h).
+
+The library is built in-tree (``thatsmyface_amd/libtmfwm.so``, see
+``thatsmyface_amd/csrc/Makefile`` / ``__graft_entry__.build()``).  There is no
+CPU fallback: if the library or a GPU is missing every call raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libtmfwm.so")
+ABI_VERSION = 1
+
+MEM_HOST = 0
+MEM_DEVICE = 1
+
+ERR_INVALID = -22
+ERR_NOMEM = -12
+ERR_HIP = -5
+ERR_UNSUPPORTED = -95
+ERR_NODEVICE = -19
+
+_u8p = ctypes.c_void_p
+_I64 = ctypes.c_int64
+_I32 = ctypes.c_int32
+_D = ctypes.c_double
+_VP = ctypes.c_void_p
+
+# name -> (restype, argtypes): exactly the entry points of include/tmfwm.h
+SIGNATURES = {
+    "tmfwm_abi_version": (ctypes.c_int, []),
+    "tmfwm_last_error": (ctypes.c_char_p, []),
+    "tmfwm_device_count": (ctypes.c_int, []),
+    "tmfwm_embed": (ctypes.c_int, [_VP, _I64, _I32, _I32, _I64, _VP, _I32, _D, _VP, _I32, _VP]),
+    "tmfwm_extract": (ctypes.c_int, [_VP, _VP, _I64, _I32, _I32, _I64, _I32, _D, _VP, _I32, _VP]),
+    "tmfwm_rgb_to_ycbcr": (ctypes.c_int, [_VP, _I64, _VP, _I32, _VP]),
+    "tmfwm_ycbcr_to_rgb": (ctypes.c_int, [_VP, _I64, _VP, _I32, _VP]),
+    "tmfwm_dct2d_blocks": (ctypes.c_int, [_VP, _I64, _I32, _I32, _I32, _VP]),
+    "tmfwm_svd_blocks": (ctypes.c_int, [_VP, _I64, _I32, _VP, _VP, _VP, _VP, _I32, _VP]),
+    "tmfwm_synth_frames": (ctypes.c_int, [ctypes.c_uint64, _I64, _I64, _I64, _VP, _VP]),
+}
+
+_lock = threading.Lock()
+_lib = None
+
+
+class TmfwmError(RuntimeError):
+    """A HIP-side failure reported by libtmfwm.so."""
+
+
+def load():
+    """Load and type the library once; raises ImportError if it was not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise ImportError(
+                    f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+                    "or `make -C thatsmyface_amd/csrc` (hipcc, gfx950)"
+                )
+            L = ctypes.CDLL(LIB_PATH)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(L, name)
+                fn.restype = res
+                fn.argtypes = args
+            v = L.tmfwm_abi_version()
+            if v != ABI_VERSION:
+                raise ImportError(f"libtmfwm ABI {v} != expected {ABI_VERSION}")
+            _lib = L
+    return _lib
+
+
+def last_error() -> str:
+    msg = load().tmfwm_last_error()
+    return msg.decode(errors="replace") if msg else ""
+
+
+def check(rc: int, what: str) -> None:
+    if rc == 0:
+        return
+    msg = f"{what}: {last_error()} (status {rc})"
+    if rc == ERR_INVALID:
+        raise ValueError(msg)
+    if rc == ERR_UNSUPPORTED:
+        raise NotImplementedError(msg)
+    raise TmfwmError(msg)
+
+
+def device_count() -> int:
+    return int(load().tmfwm_device_count())

@@ -1,0 +1,111 @@
+"""Device-resident batch API: frames already in HBM (torch tensors on a ROCm GPU).
+
+This is the path the benchmark and multi-GPU driver use: a batch of N frames
+(N, H, W, 3) uint8 on ``cuda:k`` is embedded / extracted by ONE kernel launch
+each, enqueued on the caller's current torch stream.  torch provides device
+memory and streams only; the arithmetic is libtmfwm.so's HIP kernels.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+from .constants import SUPPORTED_BLOCK_SIZES
+
+SEED_COVER = 0x5EED0001
+SEED_WATERMARK = 0x5EED0002
+
+
+def _stream(stream) -> int:
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return int(s.cuda_stream)
+
+
+def _check_frames(t: torch.Tensor, name: str) -> None:
+    if not t.is_cuda:
+        raise ValueError(f"{name} must be a GPU tensor")
+    if t.dtype != torch.uint8 or t.dim() != 4 or t.shape[-1] != 3:
+        raise ValueError(f"{name} must be (N, H, W, 3) uint8, got {tuple(t.shape)} {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+
+
+def embed_batch(frames: torch.Tensor, wm_tile: torch.Tensor, block: int = 8, alpha: float = 0.1,
+                out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+    """Embed one watermark tile into every frame (watermarking.py:135 per frame)."""
+    _check_frames(frames, "frames")
+    n, h, w, _ = frames.shape
+    if block not in SUPPORTED_BLOCK_SIZES:
+        raise NotImplementedError(f"block {block}")
+    if tuple(wm_tile.shape) != (h // block, w // block) or wm_tile.dtype != torch.uint8 or not wm_tile.is_cuda:
+        raise ValueError(f"wm_tile must be ({h // block}, {w // block}) uint8 on the GPU, got {tuple(wm_tile.shape)}")
+    wm_tile = wm_tile.contiguous()
+    if out is None:
+        out = torch.empty_like(frames)
+    else:
+        _check_frames(out, "out")
+        if out.shape != frames.shape:
+            raise ValueError("out shape mismatch")
+    with torch.cuda.device(frames.device):
+        L = _lib.load()
+        _lib.check(L.tmfwm_embed(frames.data_ptr(), n, h, w, h * w * 3, wm_tile.data_ptr(), block, float(alpha),
+                                 out.data_ptr(), _lib.MEM_DEVICE, _stream(stream)), "embed_batch")
+    return out
+
+
+def extract_batch(wframes: torch.Tensor, oframes: torch.Tensor, block: int = 8, alpha: float = 0.1,
+                  out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+    """Extract the watermark tile of every frame pair (watermarking.py:224 per pair)."""
+    _check_frames(wframes, "wframes")
+    _check_frames(oframes, "oframes")
+    if wframes.shape != oframes.shape:
+        raise ValueError("watermarked / original batch shapes differ")
+    n, h, w, _ = wframes.shape
+    if block not in SUPPORTED_BLOCK_SIZES:
+        raise NotImplementedError(f"block {block}")
+    if out is None:
+        out = torch.empty((n, h // block, w // block), dtype=torch.uint8, device=wframes.device)
+    with torch.cuda.device(wframes.device):
+        L = _lib.load()
+        _lib.check(L.tmfwm_extract(wframes.data_ptr(), oframes.data_ptr(), n, h, w, h * w * 3, block, float(alpha),
+                                   out.data_ptr(), _lib.MEM_DEVICE, _stream(stream)), "extract_batch")
+    return out
+
+
+def synth_frames(n: int, height: int, width: int, seed: int = SEED_COVER, frame0: int = 0,
+                 device: torch.device | str | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
+    """Counter-based synthetic uint8 frames generated directly in HBM."""
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    if out is None:
+        out = torch.empty((n, height, width, 3), dtype=torch.uint8, device=dev)
+    with torch.cuda.device(out.device):
+        L = _lib.load()
+        _lib.check(L.tmfwm_synth_frames(seed, frame0, n, height * width * 3, out.data_ptr(), _stream(None)), "synth_frames")
+    return out
+
+
+def synth_tile(nbh: int, nbw: int, seed: int = SEED_WATERMARK, device=None) -> torch.Tensor:
+    """Synthetic watermark tile: the same generator over an nbh x nbw byte plane."""
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    out = torch.empty((nbh, nbw), dtype=torch.uint8, device=dev)
+    with torch.cuda.device(dev):
+        L = _lib.load()
+        _lib.check(L.tmfwm_synth_frames(seed, 0, 1, nbh * nbw, out.data_ptr(), _stream(None)), "synth_tile")
+    return out
+
+
+def svd_blocks(D: torch.Tensor):
+    """SVD stage alone on (n, b, b) float32 blocks: (U, S, Vt, sweeps) as the reference consumes them."""
+    if not D.is_cuda or D.dtype != torch.float32 or D.dim() != 3 or D.shape[1] != D.shape[2]:
+        raise ValueError("D must be (n, b, b) float32 on the GPU")
+    D = D.contiguous()
+    n, b, _ = D.shape
+    U = torch.empty_like(D)
+    Vt = torch.empty_like(D)
+    S = torch.empty((n, b), dtype=torch.float32, device=D.device)
+    sw = torch.empty((n,), dtype=torch.int32, device=D.device)
+    with torch.cuda.device(D.device):
+        L = _lib.load()
+        _lib.check(L.tmfwm_svd_blocks(D.data_ptr(), n, b, U.data_ptr(), S.data_ptr(), Vt.data_ptr(), sw.data_ptr(),
+                                      _lib.MEM_DEVICE, _stream(None)), "svd_blocks")
+    return U, S, Vt, sw

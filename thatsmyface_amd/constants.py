@@ -1,0 +1,7 @@
+"""Watermark constants of the reference (modules/constants.py:7-9)."""
+
+BLOCK_SIZE = 8  # constants.py:7
+ALPHA = 0.1  # constants.py:8
+MAX_SVD_COEFFICIENTS = 10  # constants.py:9 (unused by the reference too)
+
+SUPPORTED_BLOCK_SIZES = (4, 8, 16)

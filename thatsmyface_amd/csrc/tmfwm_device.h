@@ -1,0 +1,562 @@
+// Device-side arithmetic of the watermark path for gfx950 (MI355X).
+//
+// Every function here reproduces one step of the reference numerics
+// (/root/reference/modules/watermarking.py) at the bit level; the contract is
+// SURVEY.md 8(a) N1-N10 and DESIGN.md section 3.  The TU is compiled with
+// -ffp-contract=off: every '*', '+', '-' below is one IEEE operation and fused
+// multiply-adds appear only where written (__builtin_fma / __builtin_fmaf).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <type_traits>
+#include <utility>
+
+#include "tmfwm_consts.h"
+
+#define TMF_DEVI __device__ __forceinline__
+
+namespace tmf {
+
+// ---------------------------------------------------------------------------
+// Colour (N1, N2, N9)
+// ---------------------------------------------------------------------------
+
+// f32(v) / 255.0f, correctly rounded (watermarking.py:29), as one multiply plus a
+// residual correction; exhaustively equal to the IEEE divide for v = 0..255.
+TMF_DEVI float unit_from_u8(uint32_t v)
+{
+    const float x = (float)v;
+    constexpr float r = 1.0f / 255.0f;
+    const float q = x * r;
+    const float e = __builtin_fmaf(-q, 255.0f, x);
+    return __builtin_fmaf(e, r, q);
+}
+
+// Y only (watermarking.py:37-45, row 0 of the transform; OpenBLAS dgemv FMA pattern)
+TMF_DEVI float luma(uint32_t R, uint32_t G, uint32_t B)
+{
+    const double r = unit_from_u8(R), g = unit_from_u8(G), b = unit_from_u8(B);
+    return (float)__builtin_fma(0.114, b, __builtin_fma(0.299, r, 0.587 * g));
+}
+
+// Cb, Cr as stored by rgb_to_ycbcr (f32 of the f64 dot, then "+= 0.5" in f32, :48)
+TMF_DEVI void chroma(uint32_t R, uint32_t G, uint32_t B, float &cbs, float &crs)
+{
+    const double r = unit_from_u8(R), g = unit_from_u8(G), b = unit_from_u8(B);
+    cbs = (float)__builtin_fma(0.5, b, __builtin_fma(-0.169, r, -0.331 * g)) + 0.5f;
+    crs = (float)__builtin_fma(-0.081, b, __builtin_fma(0.5, r, -0.419 * g)) + 0.5f;
+}
+
+// np.clip(.,0,1) in f32, * 255 in f32, astype(uint8) = truncation (watermarking.py:70-73)
+TMF_DEVI uint32_t u8_from_unit(float f)
+{
+    f = f < 0.0f ? 0.0f : f;
+    f = f > 1.0f ? 1.0f : f;
+    return (uint32_t)(f * 255.0f);
+}
+
+// ycbcr_to_rgb for one pixel (watermarking.py:55-73): Cb, Cr -= 0.5 in f32, then the
+// dgemv pattern fma(Ti[c][2], cr, fma(Ti[c][0], y, Ti[c][1]*cb)) in f64.
+TMF_DEVI void colour_inv(float y, float cbs, float crs, uint32_t &R, uint32_t &G, uint32_t &B)
+{
+    const double Y = y, CB = cbs - 0.5f, CR = crs - 0.5f;
+    R = u8_from_unit((float)__builtin_fma(1.403, CR, __builtin_fma(1.0, Y, 0.0 * CB)));
+    G = u8_from_unit((float)__builtin_fma(-0.714, CR, __builtin_fma(1.0, Y, -0.344 * CB)));
+    B = u8_from_unit((float)__builtin_fma(0.0, CR, __builtin_fma(1.0, Y, 1.773 * CB)));
+}
+
+// ---------------------------------------------------------------------------
+// pocketfft fp32 DCT-II / DCT-III (N3), lengths 4, 8, 16, fully unrolled on
+// register arrays.  rfftp radix passes with compile-time (ido, l1).
+// ---------------------------------------------------------------------------
+namespace dct {
+
+constexpr float kSqrt2 = 1.41421356237309504880f;
+constexpr float kHsqt2 = 0.70710678118654752440f;
+
+template <int IDO, int L1, int N>
+TMF_DEVI void radb2(const float (&cc)[N], float (&ch)[N], const float *wa)
+{
+#define CC(a, b, c) cc[(a) + IDO * ((b) + 2 * (c))]
+#define CH(a, b, c) ch[(a) + IDO * ((b) + L1 * (c))]
+#pragma unroll
+    for (int k = 0; k < L1; k++) {
+        const float x = CC(0, 0, k), y = CC(IDO - 1, 1, k);
+        CH(0, k, 0) = x + y;
+        CH(0, k, 1) = x - y;
+    }
+    if constexpr ((IDO & 1) == 0) {
+#pragma unroll
+        for (int k = 0; k < L1; k++) {
+            CH(IDO - 1, k, 0) = 2.0f * CC(IDO - 1, 0, k);
+            CH(IDO - 1, k, 1) = -2.0f * CC(0, 1, k);
+        }
+    }
+    if constexpr (IDO > 2) {
+#pragma unroll
+        for (int k = 0; k < L1; ++k)
+#pragma unroll
+            for (int i = 2; i < IDO; i += 2) {
+                const int ic = IDO - i;
+                const float a = CC(i - 1, 0, k), b = CC(ic - 1, 1, k);
+                CH(i - 1, k, 0) = a + b;
+                const float tr2 = a - b;
+                const float c = CC(i, 0, k), d = CC(ic, 1, k);
+                const float ti2 = c + d;
+                CH(i, k, 0) = c - d;
+                const float w0 = wa[i - 2], w1 = wa[i - 1];
+                CH(i, k, 1) = w0 * ti2 + w1 * tr2;
+                CH(i - 1, k, 1) = w0 * tr2 - w1 * ti2;
+            }
+    }
+#undef CC
+#undef CH
+}
+
+template <int IDO, int L1, int N>
+TMF_DEVI void radb4(const float (&cc)[N], float (&ch)[N], const float *wa)
+{
+#define CC(a, b, c) cc[(a) + IDO * ((b) + 4 * (c))]
+#define CH(a, b, c) ch[(a) + IDO * ((b) + L1 * (c))]
+#pragma unroll
+    for (int k = 0; k < L1; k++) {
+        const float x = CC(0, 0, k), y = CC(IDO - 1, 3, k);
+        const float tr2 = x + y, tr1 = x - y;
+        const float tr3 = 2.0f * CC(IDO - 1, 1, k);
+        const float tr4 = 2.0f * CC(0, 2, k);
+        CH(0, k, 0) = tr2 + tr3;
+        CH(0, k, 2) = tr2 - tr3;
+        CH(0, k, 3) = tr1 + tr4;
+        CH(0, k, 1) = tr1 - tr4;
+    }
+    if constexpr ((IDO & 1) == 0) {
+#pragma unroll
+        for (int k = 0; k < L1; k++) {
+            const float a = CC(0, 3, k), b = CC(0, 1, k);
+            const float ti1 = a + b, ti2 = a - b;
+            const float c = CC(IDO - 1, 0, k), d = CC(IDO - 1, 2, k);
+            const float tr2 = c + d, tr1 = c - d;
+            CH(IDO - 1, k, 0) = tr2 + tr2;
+            CH(IDO - 1, k, 1) = kSqrt2 * (tr1 - ti1);
+            CH(IDO - 1, k, 2) = ti2 + ti2;
+            CH(IDO - 1, k, 3) = -kSqrt2 * (tr1 + ti1);
+        }
+    }
+    if constexpr (IDO > 2) {
+#pragma unroll
+        for (int k = 0; k < L1; ++k)
+#pragma unroll
+            for (int i = 2; i < IDO; i += 2) {
+                const int ic = IDO - i;
+                float a, b;
+                a = CC(i - 1, 0, k); b = CC(ic - 1, 3, k);
+                const float tr2 = a + b, tr1 = a - b;
+                a = CC(i, 0, k); b = CC(ic, 3, k);
+                const float ti1 = a + b, ti2 = a - b;
+                a = CC(i, 2, k); b = CC(ic, 1, k);
+                const float tr4 = a + b, ti3 = a - b;
+                a = CC(i - 1, 2, k); b = CC(ic - 1, 1, k);
+                const float tr3 = a + b, ti4 = a - b;
+                CH(i - 1, k, 0) = tr2 + tr3;
+                const float cr3 = tr2 - tr3;
+                CH(i, k, 0) = ti2 + ti3;
+                const float ci3 = ti2 - ti3;
+                const float cr4 = tr1 + tr4, cr2 = tr1 - tr4;
+                const float ci2 = ti1 + ti4, ci4 = ti1 - ti4;
+                float w0 = wa[i - 2], w1 = wa[i - 1];
+                CH(i, k, 1) = w0 * ci2 + w1 * cr2;
+                CH(i - 1, k, 1) = w0 * cr2 - w1 * ci2;
+                w0 = wa[(IDO - 1) + i - 2]; w1 = wa[(IDO - 1) + i - 1];
+                CH(i, k, 2) = w0 * ci3 + w1 * cr3;
+                CH(i - 1, k, 2) = w0 * cr3 - w1 * ci3;
+                w0 = wa[2 * (IDO - 1) + i - 2]; w1 = wa[2 * (IDO - 1) + i - 1];
+                CH(i, k, 3) = w0 * ci4 + w1 * cr4;
+                CH(i - 1, k, 3) = w0 * cr4 - w1 * ci4;
+            }
+    }
+#undef CC
+#undef CH
+}
+
+template <int IDO, int L1, int N>
+TMF_DEVI void radf2(const float (&cc)[N], float (&ch)[N], const float *wa)
+{
+#define CC(a, b, c) cc[(a) + IDO * ((b) + L1 * (c))]
+#define CH(a, b, c) ch[(a) + IDO * ((b) + 2 * (c))]
+#pragma unroll
+    for (int k = 0; k < L1; k++) {
+        const float x = CC(0, k, 0), y = CC(0, k, 1);
+        CH(0, 0, k) = x + y;
+        CH(IDO - 1, 1, k) = x - y;
+    }
+    if constexpr ((IDO & 1) == 0) {
+#pragma unroll
+        for (int k = 0; k < L1; k++) {
+            CH(0, 1, k) = -CC(IDO - 1, k, 1);
+            CH(IDO - 1, 0, k) = CC(IDO - 1, k, 0);
+        }
+    }
+    if constexpr (IDO > 2) {
+#pragma unroll
+        for (int k = 0; k < L1; k++)
+#pragma unroll
+            for (int i = 2; i < IDO; i += 2) {
+                const int ic = IDO - i;
+                const float w0 = wa[i - 2], w1 = wa[i - 1];
+                const float e = CC(i - 1, k, 1), f = CC(i, k, 1);
+                const float tr2 = w0 * e + w1 * f;
+                const float ti2 = w0 * f - w1 * e;
+                const float a = CC(i - 1, k, 0);
+                CH(i - 1, 0, k) = a + tr2;
+                CH(ic - 1, 1, k) = a - tr2;
+                const float c = CC(i, k, 0);
+                CH(i, 0, k) = ti2 + c;
+                CH(ic, 1, k) = ti2 - c;
+            }
+    }
+#undef CC
+#undef CH
+}
+
+template <int IDO, int L1, int N>
+TMF_DEVI void radf4(const float (&cc)[N], float (&ch)[N], const float *wa)
+{
+#define CC(a, b, c) cc[(a) + IDO * ((b) + L1 * (c))]
+#define CH(a, b, c) ch[(a) + IDO * ((b) + 4 * (c))]
+#pragma unroll
+    for (int k = 0; k < L1; k++) {
+        float a = CC(0, k, 3), b = CC(0, k, 1);
+        const float tr1 = a + b;
+        CH(0, 2, k) = a - b;
+        a = CC(0, k, 0); b = CC(0, k, 2);
+        const float tr2 = a + b;
+        CH(IDO - 1, 1, k) = a - b;
+        CH(0, 0, k) = tr2 + tr1;
+        CH(IDO - 1, 3, k) = tr2 - tr1;
+    }
+    if constexpr ((IDO & 1) == 0) {
+#pragma unroll
+        for (int k = 0; k < L1; k++) {
+            const float ti1 = -kHsqt2 * (CC(IDO - 1, k, 1) + CC(IDO - 1, k, 3));
+            const float tr1 = kHsqt2 * (CC(IDO - 1, k, 1) - CC(IDO - 1, k, 3));
+            const float a = CC(IDO - 1, k, 0);
+            CH(IDO - 1, 0, k) = a + tr1;
+            CH(IDO - 1, 2, k) = a - tr1;
+            const float c = CC(IDO - 1, k, 2);
+            CH(0, 3, k) = ti1 + c;
+            CH(0, 1, k) = ti1 - c;
+        }
+    }
+    if constexpr (IDO > 2) {
+#pragma unroll
+        for (int k = 0; k < L1; k++)
+#pragma unroll
+            for (int i = 2; i < IDO; i += 2) {
+                const int ic = IDO - i;
+                float w0 = wa[i - 2], w1 = wa[i - 1];
+                float e = CC(i - 1, k, 1), f = CC(i, k, 1);
+                const float cr2 = w0 * e + w1 * f, ci2 = w0 * f - w1 * e;
+                w0 = wa[(IDO - 1) + i - 2]; w1 = wa[(IDO - 1) + i - 1];
+                e = CC(i - 1, k, 2); f = CC(i, k, 2);
+                const float cr3 = w0 * e + w1 * f, ci3 = w0 * f - w1 * e;
+                w0 = wa[2 * (IDO - 1) + i - 2]; w1 = wa[2 * (IDO - 1) + i - 1];
+                e = CC(i - 1, k, 3); f = CC(i, k, 3);
+                const float cr4 = w0 * e + w1 * f, ci4 = w0 * f - w1 * e;
+                const float tr1 = cr4 + cr2, tr4 = cr4 - cr2;
+                const float ti1 = ci2 + ci4, ti4 = ci2 - ci4;
+                const float a = CC(i - 1, k, 0), c = CC(i, k, 0);
+                const float tr2 = a + cr3, tr3 = a - cr3;
+                const float ti2 = c + ci3, ti3 = c - ci3;
+                CH(i - 1, 0, k) = tr2 + tr1;
+                CH(ic - 1, 3, k) = tr2 - tr1;
+                CH(i, 0, k) = ti1 + ti2;
+                CH(ic, 3, k) = ti1 - ti2;
+                CH(i - 1, 2, k) = tr3 + ti4;
+                CH(ic - 1, 1, k) = tr3 - ti4;
+                CH(i, 2, k) = tr4 + ti3;
+                CH(ic, 1, k) = tr4 - ti3;
+            }
+    }
+#undef CC
+#undef CH
+}
+
+// rfftp::exec for the factorisations pocketfft picks: 4 -> [4], 8 -> [2,4], 16 -> [4,4];
+// copy_and_norm multiplies by fct at the end.
+template <int N>
+TMF_DEVI void rfft_backward(float (&c)[N], float fct)
+{
+    float ch[N];
+    if constexpr (N == 4) {
+        radb4<1, 1>(c, ch, nullptr);
+#pragma unroll
+        for (int i = 0; i < N; ++i) c[i] = fct * ch[i];
+    } else if constexpr (N == 8) {
+        radb2<4, 1>(c, ch, kRfftTw8);
+        radb4<1, 2>(ch, c, nullptr);
+#pragma unroll
+        for (int i = 0; i < N; ++i) c[i] *= fct;
+    } else {
+        radb4<4, 1>(c, ch, kRfftTw16);
+        radb4<1, 4>(ch, c, nullptr);
+#pragma unroll
+        for (int i = 0; i < N; ++i) c[i] *= fct;
+    }
+}
+
+template <int N>
+TMF_DEVI void rfft_forward(float (&c)[N], float fct)
+{
+    float ch[N];
+    if constexpr (N == 4) {
+        radf4<1, 1>(c, ch, nullptr);
+#pragma unroll
+        for (int i = 0; i < N; ++i) c[i] = fct * ch[i];
+    } else if constexpr (N == 8) {
+        radf4<1, 2>(c, ch, nullptr);
+        radf2<4, 1>(ch, c, kRfftTw8);
+#pragma unroll
+        for (int i = 0; i < N; ++i) c[i] *= fct;
+    } else {
+        radf4<1, 4>(c, ch, nullptr);
+        radf4<4, 1>(ch, c, kRfftTw16);
+#pragma unroll
+        for (int i = 0; i < N; ++i) c[i] *= fct;
+    }
+}
+
+template <int N> struct Tw;
+template <> struct Tw<4> { static constexpr const float *d = kDctTw4; static constexpr float norm = kNorm4; };
+template <> struct Tw<8> { static constexpr const float *d = kDctTw8; static constexpr float norm = kNorm8; };
+template <> struct Tw<16> { static constexpr const float *d = kDctTw16; static constexpr float norm = kNorm16; };
+
+// T_dcst23 type 2 (scipy.fftpack.dct, norm="ortho")
+template <int N>
+TMF_DEVI void dct2(float (&c)[N])
+{
+    constexpr int NS2 = (N + 1) / 2;
+    const float *tw = Tw<N>::d;
+    c[0] *= 2.0f;
+    c[N - 1] *= 2.0f;
+#pragma unroll
+    for (int k = 1; k < N - 1; k += 2) {
+        const float t = c[k + 1];
+        c[k + 1] = t - c[k];
+        c[k] = c[k] + t;
+    }
+    rfft_backward<N>(c, Tw<N>::norm);
+#pragma unroll
+    for (int k = 1; k < NS2; ++k) {
+        const int kc = N - k;
+        const float t1 = tw[k - 1] * c[kc] + tw[kc - 1] * c[k];
+        const float t2 = tw[k - 1] * c[k] - tw[kc - 1] * c[kc];
+        c[k] = 0.5f * (t1 + t2);
+        c[kc] = 0.5f * (t1 - t2);
+    }
+    c[NS2] *= tw[NS2 - 1];
+    c[0] *= kSqrt2 * 0.5f;
+}
+
+// T_dcst23 type 3 (scipy.fftpack.idct, norm="ortho")
+template <int N>
+TMF_DEVI void dct3(float (&c)[N])
+{
+    constexpr int NS2 = (N + 1) / 2;
+    const float *tw = Tw<N>::d;
+    c[0] *= kSqrt2;
+#pragma unroll
+    for (int k = 1; k < NS2; ++k) {
+        const int kc = N - k;
+        const float t1 = c[k] + c[kc], t2 = c[k] - c[kc];
+        c[k] = tw[k - 1] * t2 + tw[kc - 1] * t1;
+        c[kc] = tw[k - 1] * t1 - tw[kc - 1] * t2;
+    }
+    c[NS2] *= 2.0f * tw[NS2 - 1];
+    rfft_forward<N>(c, Tw<N>::norm);
+#pragma unroll
+    for (int k = 1; k < N - 1; k += 2) {
+        const float t = c[k];
+        c[k] = t - c[k + 1];
+        c[k + 1] = t + c[k + 1];
+    }
+}
+
+}  // namespace dct
+
+// ---------------------------------------------------------------------------
+// Jacobi SVD (N5/N6) with B/L rows of A and V per lane, L lanes per block.
+// The op sequence is the oracle's: dot products are fma chains
+// over each lane's R contiguous rows, combined across the L lanes by an xor
+// butterfly (== balanced pairwise tree); round-robin pair schedule; rotation
+// iff g^2 > TOL2*a*b and g^2 > C*(a+b).
+// ---------------------------------------------------------------------------
+constexpr int kMaxSweeps = 32;
+constexpr double kTol2 = 7.888609052210118e-31;  // 2^-100
+constexpr double kC2 = 9.860761315262648e-32;    // 2^-103
+
+// circle-method schedule: L = [0, 1 + (k-1+s) mod (b-1)], pair p = (L[p], L[b-1-p]) sorted
+template <int B>
+struct Sched {
+    static constexpr int idx(int s, int k) { return k == 0 ? 0 : 1 + ((k - 1 + s) % (B - 1)); }
+    static constexpr int lo(int s, int p) { return idx(s, p) < idx(s, B - 1 - p) ? idx(s, p) : idx(s, B - 1 - p); }
+    static constexpr int hi(int s, int p) { return idx(s, p) < idx(s, B - 1 - p) ? idx(s, B - 1 - p) : idx(s, p); }
+};
+
+// ---- compile-time loops (guaranteed unrolling: register arrays need constant indices)
+template <typename F, int... Is>
+TMF_DEVI void static_for_impl(F &&f, std::integer_sequence<int, Is...>)
+{
+    (f(std::integral_constant<int, Is>{}), ...);
+}
+template <int N, typename F>
+TMF_DEVI void static_for(F &&f)
+{
+    static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+// ---- cross-lane moves inside a block group (DPP / ds_swizzle, no LDS traffic)
+template <int CTRL>
+TMF_DEVI double dpp_d(double v)
+{
+    const long long b = __builtin_bit_cast(long long, v);
+    const int lo = __builtin_amdgcn_mov_dpp((int)b, CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xF, 0xF, false);
+    return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+}
+template <int PATTERN>
+TMF_DEVI double swz_d(double v)
+{
+    const long long b = __builtin_bit_cast(long long, v);
+    const int lo = __builtin_amdgcn_ds_swizzle((int)b, PATTERN);
+    const int hi = __builtin_amdgcn_ds_swizzle((int)(b >> 32), PATTERN);
+    return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+}
+template <int CTRL>
+TMF_DEVI int dpp_i(int v) { return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, false); }
+template <int PATTERN>
+TMF_DEVI int swz_i(int v) { return __builtin_amdgcn_ds_swizzle(v, PATTERN); }
+
+// DPP controls: quad_perm [1,0,3,2] = 0xB1 (xor 1), [2,3,0,1] = 0x4E (xor 2),
+// row_half_mirror = 0x141 (lane i <-> 7-i within 8 lanes).
+// Butterfly sum over the L lanes of a group == the oracle's pairwise tree:
+// level 3 pairs lane i with 7-i, whose value (p6+p7)+(p4+p5) equals (p4+p5)+(p6+p7) bitwise.
+template <int L>
+TMF_DEVI double group_sum(double v)
+{
+    static_assert(L == 1 || L == 2 || L == 4 || L == 8, "group size");
+    if constexpr (L >= 2) v = v + dpp_d<0xB1>(v);
+    if constexpr (L >= 4) v = v + dpp_d<0x4E>(v);
+    if constexpr (L >= 8) v = v + dpp_d<0x141>(v);
+    return v;
+}
+
+// value of lane (group base + K) for every lane of the group
+template <int L, int K>
+TMF_DEVI double group_bcast(double v)
+{
+    if constexpr (L == 1) return v;
+    else if constexpr (L == 2) return dpp_d<K == 0 ? 0xA0 : 0xF5>(v);                    // quad_perm [K,K,K+2,K+2]
+    else if constexpr (L == 4) return dpp_d<K | (K << 2) | (K << 4) | (K << 6)>(v);      // quad_perm [K,K,K,K]
+    else return swz_d<(K << 5) | 0x18>(v);                                                // bitmask: (lane & 0x18) | K
+}
+template <int L, int K>
+TMF_DEVI int group_bcast_i(int v)
+{
+    if constexpr (L == 1) return v;
+    else if constexpr (L == 2) return dpp_i<K == 0 ? 0xA0 : 0xF5>(v);
+    else if constexpr (L == 4) return dpp_i<K | (K << 2) | (K << 4) | (K << 6)>(v);
+    else return swz_i<(K << 5) | 0x18>(v);
+}
+
+// sum over rows of A[:,i]*A[:,j] in the contract order
+template <int R, int B, int L>
+TMF_DEVI double cdot(const double (&A)[R][B], int i, int j)
+{
+    double acc = 0.0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc = __builtin_fma(A[r][i], A[r][j], acc);
+    return group_sum<L>(acc);
+}
+
+struct Rot {
+    double c, s;
+    int on;
+};
+
+TMF_DEVI Rot rotation(double alpha, double beta, double gamma, double c2)
+{
+    Rot r;
+    const double g2 = gamma * gamma;
+    r.on = !(g2 <= c2 * (alpha + beta) || g2 <= (kTol2 * alpha) * beta);
+    const double zeta = (beta - alpha) / (2.0 * gamma);
+    const double t = __builtin_copysign(1.0, zeta) / (__builtin_fabs(zeta) + __builtin_sqrt(__builtin_fma(zeta, zeta, 1.0)));
+    r.c = 1.0 / __builtin_sqrt(__builtin_fma(t, t, 1.0));
+    r.s = r.c * t;
+    return r;
+}
+
+// One-sided Jacobi on A (and V when WANT_V).  Returns sweeps executed by the wave.
+// Pairs of a round are disjoint, so they are applied in any order; lane q of a group
+// evaluates the rotations of pairs [q*PP, q*PP+PP) and broadcasts them.
+template <int B, int L, bool WANT_V>
+TMF_DEVI int jacobi(double (&A)[B / L][B], double (&V)[B / L][B], int q)
+{
+    constexpr int R = B / L, NP = B / 2, PP = NP / L;
+    static_assert(PP >= 1, "need L <= B/2");
+    double F = 0.0;
+    static_for<B>([&](auto K) { F += cdot<R, B, L>(A, K, K); });
+    const double c2 = kC2 * F;
+    int sweep = 0;
+    for (; sweep < kMaxSweeps; ++sweep) {
+        int rotated = 0;
+        static_for<B - 1>([&](auto S) {
+            constexpr int s = S;
+            // alpha, beta, gamma of the pairs this lane evaluates
+            double al[PP], be[PP], ga[PP];
+            static_for<NP>([&](auto P) {
+                constexpr int p = P, i = Sched<B>::lo(s, p), j = Sched<B>::hi(s, p), u = p % PP;
+                const double a = cdot<R, B, L>(A, i, i);
+                const double b = cdot<R, B, L>(A, j, j);
+                const double g = cdot<R, B, L>(A, i, j);
+                if (p / PP == 0 || p / PP == q) {
+                    al[u] = a;
+                    be[u] = b;
+                    ga[u] = g;
+                }
+            });
+            Rot mine[PP];
+            static_for<PP>([&](auto U) { mine[U] = rotation(al[U], be[U], ga[U], c2); });
+            static_for<NP>([&](auto P) {
+                constexpr int p = P, i = Sched<B>::lo(s, p), j = Sched<B>::hi(s, p), u = p % PP, src = p / PP;
+                const double c = group_bcast<L, src>(mine[u].c);
+                const double sn = group_bcast<L, src>(mine[u].s);
+                const int on = group_bcast_i<L, src>(mine[u].on);
+                if (on) {
+                    rotated = 1;
+#pragma unroll
+                    for (int r = 0; r < R; ++r) {
+                        const double x = A[r][i], y = A[r][j];
+                        A[r][i] = __builtin_fma(-sn, y, c * x);
+                        A[r][j] = __builtin_fma(sn, x, c * y);
+                    }
+                    if constexpr (WANT_V) {
+#pragma unroll
+                        for (int r = 0; r < R; ++r) {
+                            const double x = V[r][i], y = V[r][j];
+                            V[r][i] = __builtin_fma(-sn, y, c * x);
+                            V[r][j] = __builtin_fma(sn, x, c * y);
+                        }
+                    }
+                }
+            });
+        });
+        if (!__any(rotated)) {
+            ++sweep;
+            break;
+        }
+    }
+    return sweep;
+}
+
+}  // namespace tmf

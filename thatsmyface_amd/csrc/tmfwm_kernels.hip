@@ -1,0 +1,639 @@
+// HIP kernels of the watermark path for gfx950 (MI355X).
+//
+// Layout in HBM: frames are H x W x 3 u8, HWC-interleaved (PIL / numpy order), frame
+// i at base + i * frame_stride.  The watermark tile is (H/b) x (W/b) u8 shared by
+// every frame of a batch.  Extracted tiles are (H/b) x (W/b) u8 per frame.
+//
+// Work decomposition: a workgroup is ONE wave of 64 lanes that owns a
+// strip of 64/L horizontally adjacent b x b blocks of one block row of one frame;
+// L lanes cooperate on each block, lane q of a block group holding rows
+// [q*R, q*R + R) (R = b / L) of the block's pixels, of A = D*V and of V.
+// Transposes for the column passes of the DCT / IDCT go through a padded LDS tile.
+// Nothing is written to HBM between the uint8 load and the uint8 store.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "tmfwm_device.h"
+#include "tmfwm_internal.h"
+
+namespace tmf {
+
+template <int B>
+struct Geo {
+    static constexpr int L = (B == 16) ? 8 : (B == 8) ? 2 : 1;  // lanes per block (== oracle jac_chunks)
+    static constexpr int R = B / L;                              // rows per lane
+    static constexpr int BPW = 64 / L;                           // blocks per wave
+    static constexpr int NW = B * 3 / 4;                         // u32 words per pixel row of a block
+    static constexpr int STRIP_PX = BPW * B;                     // strip width in pixels
+};
+
+// ---- byte rows -------------------------------------------------------------
+template <int NW>
+TMF_DEVI void load_words(const uint8_t *p, bool aligned, uint32_t (&w)[NW])
+{
+    if (aligned) {
+        const uint32_t *q = reinterpret_cast<const uint32_t *>(p);
+#pragma unroll
+        for (int i = 0; i < NW; ++i) w[i] = q[i];
+    } else {
+#pragma unroll
+        for (int i = 0; i < NW; ++i)
+            w[i] = (uint32_t)p[4 * i] | ((uint32_t)p[4 * i + 1] << 8) | ((uint32_t)p[4 * i + 2] << 16) | ((uint32_t)p[4 * i + 3] << 24);
+    }
+}
+
+template <int NW>
+TMF_DEVI void store_words(uint8_t *p, bool aligned, const uint32_t (&w)[NW])
+{
+    if (aligned) {
+        uint32_t *q = reinterpret_cast<uint32_t *>(p);
+#pragma unroll
+        for (int i = 0; i < NW; ++i) q[i] = w[i];
+    } else {
+#pragma unroll
+        for (int i = 0; i < NW; ++i) {
+            p[4 * i] = (uint8_t)w[i];
+            p[4 * i + 1] = (uint8_t)(w[i] >> 8);
+            p[4 * i + 2] = (uint8_t)(w[i] >> 16);
+            p[4 * i + 3] = (uint8_t)(w[i] >> 24);
+        }
+    }
+}
+
+TMF_DEVI uint32_t byte_at(const uint32_t *w, int k) { return (w[k >> 2] >> (8 * (k & 3))) & 0xFFu; }
+
+// ---- LDS-mediated 2-D transforms on a block held in rows layout ---------------
+// tile: this block's [B][B+1] LDS region.  x: this lane's R rows.  Column pass
+// first (axis 0), then rows (watermarking.py:76-83).
+template <int B, bool INVERSE>
+TMF_DEVI void dct2d_rows_layout(float (&x)[Geo<B>::R][B], float *tile, int q)
+{
+    constexpr int R = Geo<B>::R, LD = B + 1;
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int c = 0; c < B; ++c) tile[(q * R + r) * LD + c] = x[r][c];
+    __syncthreads();
+    // column pass: this lane takes columns [q*R, q*R+R)
+#pragma unroll
+    for (int cc = 0; cc < R; ++cc) {
+        float col[B];
+#pragma unroll
+        for (int r = 0; r < B; ++r) col[r] = tile[r * LD + q * R + cc];
+        if constexpr (INVERSE) dct::dct3<B>(col); else dct::dct2<B>(col);
+#pragma unroll
+        for (int r = 0; r < B; ++r) tile[r * LD + q * R + cc] = col[r];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        float row[B];
+#pragma unroll
+        for (int c = 0; c < B; ++c) row[c] = tile[(q * R + r) * LD + c];
+        if constexpr (INVERSE) dct::dct3<B>(row); else dct::dct2<B>(row);
+#pragma unroll
+        for (int c = 0; c < B; ++c) x[r][c] = row[c];
+    }
+    __syncthreads();
+}
+
+struct StripPos {
+    int64_t frame;
+    int bi, bj;
+    bool valid;
+};
+
+template <int B>
+TMF_DEVI StripPos strip_pos(int strips_per_row, int nbw)
+{
+    StripPos p;
+    const int strip = blockIdx.x % strips_per_row;
+    p.bi = blockIdx.x / strips_per_row;
+    p.frame = blockIdx.y;
+    const int g = (threadIdx.x & 63) / Geo<B>::L;
+    p.bj = strip * Geo<B>::BPW + g;
+    p.valid = p.bj < nbw;
+    return p;
+}
+
+// Load this lane's R pixel rows of its block (garbage-free zeros for blocks past
+// the right edge of the block grid) and return luma rows.
+template <int B>
+TMF_DEVI void load_block_rows(const uint8_t *frame_base, int W, const StripPos &pos, int q, bool aligned,
+                              uint32_t (&words)[Geo<B>::R][Geo<B>::NW])
+{
+    constexpr int R = Geo<B>::R;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        if (pos.valid) {
+            const uint8_t *p = frame_base + ((int64_t)(pos.bi * B + q * R + r) * W + (int64_t)pos.bj * B) * 3;
+            load_words<Geo<B>::NW>(p, aligned, words[r]);
+        } else {
+#pragma unroll
+            for (int i = 0; i < Geo<B>::NW; ++i) words[r][i] = 0u;
+        }
+    }
+}
+
+template <int B>
+TMF_DEVI void luma_rows(const uint32_t (&words)[Geo<B>::R][Geo<B>::NW], float (&y)[Geo<B>::R][B])
+{
+#pragma unroll
+    for (int r = 0; r < Geo<B>::R; ++r)
+#pragma unroll
+        for (int c = 0; c < B; ++c)
+            y[r][c] = luma(byte_at(words[r], 3 * c), byte_at(words[r], 3 * c + 1), byte_at(words[r], 3 * c + 2));
+}
+
+// ---------------------------------------------------------------------------
+// Embed: watermarking.py:163-216 fused, one launch per batch.
+// ---------------------------------------------------------------------------
+template <int B>
+__global__ __launch_bounds__(64) void embed_kernel(EmbedArgs a)
+{
+    constexpr int L = Geo<B>::L, R = Geo<B>::R, BPW = Geo<B>::BPW, LD = B + 1;
+    __shared__ float lds[BPW * B * LD];
+    const int lane = threadIdx.x & 63, g = lane / L, q = lane % L;
+    float *tile = lds + g * B * LD;
+    const StripPos pos = strip_pos<B>(a.strips_per_row, a.nbw);
+    const uint8_t *src = a.src + pos.frame * a.frame_stride;
+    uint8_t *dst = a.dst + pos.frame * a.frame_stride;
+
+    uint32_t words[R][Geo<B>::NW];
+    load_block_rows<B>(src, a.W, pos, q, a.aligned, words);
+    float x[R][B];
+    luma_rows<B>(words, x);
+    dct2d_rows_layout<B, false>(x, tile, q);  // :192
+
+    double A[R][B], V[R][B];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int c = 0; c < B; ++c) {
+            A[r][c] = (double)x[r][c];
+            V[r][c] = (q * R + r == c) ? 1.0 : 0.0;
+        }
+    jacobi<B, L, true>(A, V, q);  // :195 (SVD)
+
+    // singular values, U = A / sigma, sort descending (oracle orc_svd_block)
+    double sig[B];
+    float U[R][B], Vf[R][B];
+#pragma unroll
+    for (int k = 0; k < B; ++k) {
+        sig[k] = __builtin_sqrt(cdot<R, B, L>(A, k, k));
+        const double inv = 1.0 / sig[k];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            U[r][k] = sig[k] == 0.0 ? 0.0f : (float)(A[r][k] * inv);
+            Vf[r][k] = (float)V[r][k];
+        }
+    }
+    bool zero = true;
+#pragma unroll
+    for (int k = 0; k < B; ++k) zero = zero && (sig[k] == 0.0);
+    if (zero) {  // N6: D == 0 -> U = I, Vt = I
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int k = 0; k < B; ++k) U[r][k] = Vf[r][k] = (q * R + r == k) ? 1.0f : 0.0f;
+    }
+#pragma unroll
+    for (int round = 0; round < B; ++round)
+#pragma unroll
+        for (int k = round & 1; k + 1 < B; k += 2) {
+            const bool sw = sig[k] < sig[k + 1];
+            const double s0 = sig[k], s1 = sig[k + 1];
+            sig[k] = sw ? s1 : s0;
+            sig[k + 1] = sw ? s0 : s1;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const float u0 = U[r][k], u1 = U[r][k + 1], v0 = Vf[r][k], v1 = Vf[r][k + 1];
+                U[r][k] = sw ? u1 : u0;
+                U[r][k + 1] = sw ? u0 : u1;
+                Vf[r][k] = sw ? v1 : v0;
+                Vf[r][k + 1] = sw ? v0 : v1;
+            }
+        }
+
+    // N7 blend (:198): S[0] = f32(f64(S[0]) + alpha * (w / 255.0))
+    float S[B];
+#pragma unroll
+    for (int k = 0; k < B; ++k) S[k] = (float)sig[k];
+    const uint32_t wv = pos.valid ? a.wm[(int64_t)pos.bi * a.nbw + pos.bj] : 0u;
+    S[0] = (float)((double)S[0] + a.alpha * ((double)wv / 255.0));
+
+    // N8 (:201): Bm[k][j] = S'[k] * Vt[k][j] (this lane's rows j of V), then M = U @ Bm
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int k = 0; k < B; ++k) tile[k * LD + q * R + r] = S[k] * Vf[r][k];
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        float m[B];
+#pragma unroll
+        for (int j = 0; j < B; ++j) m[j] = 0.0f;
+#pragma unroll
+        for (int k = 0; k < B; ++k)
+#pragma unroll
+            for (int j = 0; j < B; ++j) m[j] = __builtin_fmaf(U[r][k], tile[k * LD + j], m[j]);
+#pragma unroll
+        for (int j = 0; j < B; ++j) x[r][j] = m[j];
+    }
+    __syncthreads();
+    dct2d_rows_layout<B, true>(x, tile, q);  // :204
+
+    // :207-216 write back and ycbcr_to_rgb with this lane's original chroma
+    if (pos.valid) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            uint32_t out[Geo<B>::NW];
+#pragma unroll
+            for (int i = 0; i < Geo<B>::NW; ++i) out[i] = 0u;
+#pragma unroll
+            for (int c = 0; c < B; ++c) {
+                float cbs, crs;
+                chroma(byte_at(words[r], 3 * c), byte_at(words[r], 3 * c + 1), byte_at(words[r], 3 * c + 2), cbs, crs);
+                uint32_t R8, G8, B8;
+                colour_inv(x[r][c], cbs, crs, R8, G8, B8);
+                const int k0 = 3 * c;
+                out[k0 >> 2] |= R8 << (8 * (k0 & 3));
+                out[(k0 + 1) >> 2] |= G8 << (8 * ((k0 + 1) & 3));
+                out[(k0 + 2) >> 2] |= B8 << (8 * ((k0 + 2) & 3));
+            }
+            uint8_t *p = dst + ((int64_t)(pos.bi * B + q * R + r) * a.W + (int64_t)pos.bj * B) * 3;
+            store_words<Geo<B>::NW>(p, a.aligned, out);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Extract: watermarking.py:241-289 fused; sigma_1 of both images per block.
+// ---------------------------------------------------------------------------
+template <int B>
+TMF_DEVI double sigma1_of(const uint8_t *frame_base, int W, const StripPos &pos, int q, bool aligned, float *tile)
+{
+    constexpr int L = Geo<B>::L, R = Geo<B>::R;
+    uint32_t words[R][Geo<B>::NW];
+    load_block_rows<B>(frame_base, W, pos, q, aligned, words);
+    float x[R][B];
+    luma_rows<B>(words, x);
+    dct2d_rows_layout<B, false>(x, tile, q);
+    double A[R][B], V[R][B];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int c = 0; c < B; ++c) A[r][c] = (double)x[r][c];
+    jacobi<B, L, false>(A, V, q);
+    double m = 0.0;
+#pragma unroll
+    for (int k = 0; k < B; ++k) {
+        const double s = __builtin_sqrt(cdot<R, B, L>(A, k, k));
+        m = s > m ? s : m;
+    }
+    return m;
+}
+
+template <int B>
+__global__ __launch_bounds__(64) void extract_kernel(ExtractArgs a)
+{
+    constexpr int L = Geo<B>::L, BPW = Geo<B>::BPW, LD = B + 1;
+    __shared__ float lds[BPW * B * LD];
+    const int lane = threadIdx.x & 63, g = lane / L, q = lane % L;
+    float *tile = lds + g * B * LD;
+    const StripPos pos = strip_pos<B>(a.strips_per_row, a.nbw);
+    const float sw = (float)sigma1_of<B>(a.wsrc + pos.frame * a.frame_stride, a.W, pos, q, a.aligned, tile);
+    const float so = (float)sigma1_of<B>(a.osrc + pos.frame * a.frame_stride, a.W, pos, q, a.aligned, tile);
+    // :285 under numpy-2 NEP 50: (f32 - f32) / f32(alpha) in f32; :288-289 clip, *255 in f64, trunc
+    const float e = (sw - so) / a.alpha32;
+    double d = (double)e;
+    d = d < 0.0 ? 0.0 : d;
+    d = d > 1.0 ? 1.0 : d;
+    if (pos.valid && q == 0) a.out[pos.frame * a.tile_stride + (int64_t)pos.bi * a.nbw + pos.bj] = (uint8_t)(uint32_t)(d * 255.0);
+}
+
+// ---------------------------------------------------------------------------
+// Pixels outside the full-block grid only get the colour round trip (:166, :216).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void edge_roundtrip_kernel(EdgeArgs a)
+{
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t right = (int64_t)a.core_h * a.edge_w;  // right strip: rows [0,core_h), cols [core_w, W)
+    const int64_t bottom = (int64_t)(a.H - a.core_h) * a.W;
+    if (idx >= right + bottom) return;
+    int y, x;
+    if (idx < right) {
+        y = (int)(idx / a.edge_w);
+        x = a.core_w + (int)(idx % a.edge_w);
+    } else {
+        const int64_t k = idx - right;
+        y = a.core_h + (int)(k / a.W);
+        x = (int)(k % a.W);
+    }
+    const int64_t off = blockIdx.y * a.frame_stride + ((int64_t)y * a.W + x) * 3;
+    const uint32_t r = a.src[off], g = a.src[off + 1], b = a.src[off + 2];
+    float cbs, crs;
+    chroma(r, g, b, cbs, crs);
+    uint32_t R8, G8, B8;
+    colour_inv(luma(r, g, b), cbs, crs, R8, G8, B8);
+    a.dst[off] = (uint8_t)R8;
+    a.dst[off + 1] = (uint8_t)G8;
+    a.dst[off + 2] = (uint8_t)B8;
+}
+
+// ---------------------------------------------------------------------------
+// Module-level helpers of the reference API (rgb_to_ycbcr :23, ycbcr_to_rgb :53,
+// apply_dct_to_block :76, apply_idct_to_block :81) and the SVD stage on its own.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void rgb_to_ycbcr_kernel(const uint8_t *__restrict__ rgb, int64_t npix, float *__restrict__ ycc)
+{
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= npix) return;
+    const uint32_t r = rgb[3 * p], g = rgb[3 * p + 1], b = rgb[3 * p + 2];
+    float cbs, crs;
+    chroma(r, g, b, cbs, crs);
+    ycc[3 * p] = luma(r, g, b);
+    ycc[3 * p + 1] = cbs;
+    ycc[3 * p + 2] = crs;
+}
+
+__global__ __launch_bounds__(256) void ycbcr_to_rgb_kernel(const float *__restrict__ ycc, int64_t npix, uint8_t *__restrict__ rgb)
+{
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= npix) return;
+    uint32_t R8, G8, B8;
+    colour_inv(ycc[3 * p], ycc[3 * p + 1], ycc[3 * p + 2], R8, G8, B8);
+    rgb[3 * p] = (uint8_t)R8;
+    rgb[3 * p + 1] = (uint8_t)G8;
+    rgb[3 * p + 2] = (uint8_t)B8;
+}
+
+template <int B, bool INVERSE>
+__global__ __launch_bounds__(64) void dct2d_blocks_kernel(float *blocks, int64_t nblocks)
+{
+    constexpr int L = Geo<B>::L, R = Geo<B>::R, BPW = Geo<B>::BPW, LD = B + 1;
+    __shared__ float lds[BPW * B * LD];
+    const int lane = threadIdx.x & 63, g = lane / L, q = lane % L;
+    const int64_t blk = (int64_t)blockIdx.x * BPW + g;
+    const bool valid = blk < nblocks;
+    float x[R][B];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int c = 0; c < B; ++c) x[r][c] = valid ? blocks[blk * B * B + (q * R + r) * B + c] : 0.0f;
+    dct2d_rows_layout<B, INVERSE>(x, lds + g * B * LD, q);
+    if (valid)
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int c = 0; c < B; ++c) blocks[blk * B * B + (q * R + r) * B + c] = x[r][c];
+}
+
+template <int B>
+__global__ __launch_bounds__(64) void svd_blocks_kernel(const float *__restrict__ D, int64_t nblocks, float *__restrict__ U,
+                                                        float *__restrict__ S, float *__restrict__ Vt, int32_t *__restrict__ sweeps)
+{
+    constexpr int L = Geo<B>::L, R = Geo<B>::R, BPW = Geo<B>::BPW;
+    const int lane = threadIdx.x & 63, g = lane / L, q = lane % L;
+    const int64_t blk = (int64_t)blockIdx.x * BPW + g;
+    const bool valid = blk < nblocks;
+    double A[R][B], V[R][B];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int c = 0; c < B; ++c) {
+            A[r][c] = valid ? (double)D[blk * B * B + (q * R + r) * B + c] : 0.0;
+            V[r][c] = (q * R + r == c) ? 1.0 : 0.0;
+        }
+    const int nsw = jacobi<B, L, true>(A, V, q);
+    double sig[B];
+    float Uf[R][B], Vf[R][B];
+#pragma unroll
+    for (int k = 0; k < B; ++k) {
+        sig[k] = __builtin_sqrt(cdot<R, B, L>(A, k, k));
+        const double inv = 1.0 / sig[k];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            Uf[r][k] = sig[k] == 0.0 ? 0.0f : (float)(A[r][k] * inv);
+            Vf[r][k] = (float)V[r][k];
+        }
+    }
+    bool zero = true;
+#pragma unroll
+    for (int k = 0; k < B; ++k) zero = zero && (sig[k] == 0.0);
+    if (zero) {
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int k = 0; k < B; ++k) Uf[r][k] = Vf[r][k] = (q * R + r == k) ? 1.0f : 0.0f;
+    }
+#pragma unroll
+    for (int round = 0; round < B; ++round)
+#pragma unroll
+        for (int k = round & 1; k + 1 < B; k += 2) {
+            const bool sw = sig[k] < sig[k + 1];
+            const double s0 = sig[k], s1 = sig[k + 1];
+            sig[k] = sw ? s1 : s0;
+            sig[k + 1] = sw ? s0 : s1;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const float u0 = Uf[r][k], u1 = Uf[r][k + 1], v0 = Vf[r][k], v1 = Vf[r][k + 1];
+                Uf[r][k] = sw ? u1 : u0;
+                Uf[r][k + 1] = sw ? u0 : u1;
+                Vf[r][k] = sw ? v1 : v0;
+                Vf[r][k + 1] = sw ? v0 : v1;
+            }
+        }
+    if (!valid) return;
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int k = 0; k < B; ++k) {
+            U[blk * B * B + (q * R + r) * B + k] = Uf[r][k];
+            Vt[blk * B * B + k * B + q * R + r] = Vf[r][k];
+        }
+    if (q == 0) {
+#pragma unroll
+        for (int k = 0; k < B; ++k) S[blk * B + k] = (float)sig[k];
+        if (sweeps) sweeps[blk] = nsw;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Synthetic frames for the benchmark, generated in HBM:
+// byte = splitmix64(seed ^ (frame << 40) ^ idx) & 0xFF.
+// ---------------------------------------------------------------------------
+TMF_DEVI uint64_t splitmix64(uint64_t x)
+{
+    x += 0x9E3779B97F4A7C15ULL;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
+    return x ^ (x >> 31);
+}
+
+__global__ __launch_bounds__(256) void synth_kernel(uint64_t seed, int64_t frame0, int64_t frame_bytes, uint8_t *out)
+{
+    const int64_t f = blockIdx.y;
+    const uint64_t fs = seed ^ ((uint64_t)(frame0 + f) << 40);
+    uint8_t *o = out + f * frame_bytes;
+    for (int64_t i4 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i4 < frame_bytes; i4 += (int64_t)gridDim.x * blockDim.x * 4) {
+        if (i4 + 4 <= frame_bytes && ((reinterpret_cast<uintptr_t>(o + i4) & 3) == 0)) {
+            uint32_t w = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) w |= (uint32_t)(splitmix64(fs ^ (uint64_t)(i4 + k)) & 0xFF) << (8 * k);
+            *reinterpret_cast<uint32_t *>(o + i4) = w;
+        } else {
+            for (int64_t i = i4; i < i4 + 4 && i < frame_bytes; ++i) o[i] = (uint8_t)(splitmix64(fs ^ (uint64_t)i) & 0xFF);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Launchers (host side of this TU)
+// ---------------------------------------------------------------------------
+template <int B>
+static hipError_t launch_embed_b(EmbedArgs a, hipStream_t st)
+{
+    a.strips_per_row = (a.nbw + Geo<B>::BPW - 1) / Geo<B>::BPW;
+    const int64_t gx = (int64_t)a.strips_per_row * a.nbh;
+    for (int64_t f0 = 0; f0 < a.nframes; f0 += 65535) {
+        EmbedArgs c = a;
+        const int64_t nf = a.nframes - f0 < 65535 ? a.nframes - f0 : 65535;
+        c.src = a.src + f0 * a.frame_stride;
+        c.dst = a.dst + f0 * a.frame_stride;
+        hipLaunchKernelGGL(embed_kernel<B>, dim3((unsigned)gx, (unsigned)nf), dim3(64), 0, st, c);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_embed(const EmbedArgs &a, hipStream_t st)
+{
+    hipError_t e = hipSuccess;
+    if (a.nbh > 0 && a.nbw > 0) {
+        switch (a.block) {
+        case 4: e = launch_embed_b<4>(a, st); break;
+        case 8: e = launch_embed_b<8>(a, st); break;
+        case 16: e = launch_embed_b<16>(a, st); break;
+        default: return hipErrorInvalidValue;
+        }
+        if (e != hipSuccess) return e;
+    }
+    return launch_edges(a.src, a.dst, a.nframes, a.H, a.W, a.frame_stride, a.block, st);
+}
+
+hipError_t launch_edges(const uint8_t *src, uint8_t *dst, int64_t nframes, int H, int W, int64_t frame_stride, int block, hipStream_t st)
+{
+    EdgeArgs e;
+    e.src = src;
+    e.dst = dst;
+    e.H = H;
+    e.W = W;
+    e.frame_stride = frame_stride;
+    e.core_h = (H / block) * block;
+    e.core_w = (W / block) * block;
+    e.edge_w = W - e.core_w;
+    const int64_t n = (int64_t)e.core_h * e.edge_w + (int64_t)(H - e.core_h) * W;
+    if (n == 0) return hipSuccess;
+    for (int64_t f0 = 0; f0 < nframes; f0 += 65535) {
+        EdgeArgs c = e;
+        c.src = src + f0 * frame_stride;
+        c.dst = dst + f0 * frame_stride;
+        const int64_t nf = nframes - f0 < 65535 ? nframes - f0 : 65535;
+        hipLaunchKernelGGL(edge_roundtrip_kernel, dim3((unsigned)((n + 255) / 256), (unsigned)nf), dim3(256), 0, st, c);
+    }
+    return hipGetLastError();
+}
+
+template <int B>
+static hipError_t launch_extract_b(ExtractArgs a, hipStream_t st)
+{
+    a.strips_per_row = (a.nbw + Geo<B>::BPW - 1) / Geo<B>::BPW;
+    const int64_t gx = (int64_t)a.strips_per_row * a.nbh;
+    for (int64_t f0 = 0; f0 < a.nframes; f0 += 65535) {
+        ExtractArgs c = a;
+        const int64_t nf = a.nframes - f0 < 65535 ? a.nframes - f0 : 65535;
+        c.wsrc = a.wsrc + f0 * a.frame_stride;
+        c.osrc = a.osrc + f0 * a.frame_stride;
+        c.out = a.out + f0 * a.tile_stride;
+        hipLaunchKernelGGL(extract_kernel<B>, dim3((unsigned)gx, (unsigned)nf), dim3(64), 0, st, c);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_extract(const ExtractArgs &a, hipStream_t st)
+{
+    if (a.nbh == 0 || a.nbw == 0) return hipSuccess;
+    switch (a.block) {
+    case 4: return launch_extract_b<4>(a, st);
+    case 8: return launch_extract_b<8>(a, st);
+    case 16: return launch_extract_b<16>(a, st);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_rgb_to_ycbcr(const uint8_t *rgb, int64_t npix, float *ycc, hipStream_t st)
+{
+    if (npix == 0) return hipSuccess;
+    hipLaunchKernelGGL(rgb_to_ycbcr_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, st, rgb, npix, ycc);
+    return hipGetLastError();
+}
+
+hipError_t launch_ycbcr_to_rgb(const float *ycc, int64_t npix, uint8_t *rgb, hipStream_t st)
+{
+    if (npix == 0) return hipSuccess;
+    hipLaunchKernelGGL(ycbcr_to_rgb_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, st, ycc, npix, rgb);
+    return hipGetLastError();
+}
+
+template <int B>
+static hipError_t launch_dct_b(float *blocks, int64_t nb, int inverse, hipStream_t st)
+{
+    const unsigned grid = (unsigned)((nb + Geo<B>::BPW - 1) / Geo<B>::BPW);
+    if (inverse) hipLaunchKernelGGL((dct2d_blocks_kernel<B, true>), dim3(grid), dim3(64), 0, st, blocks, nb);
+    else hipLaunchKernelGGL((dct2d_blocks_kernel<B, false>), dim3(grid), dim3(64), 0, st, blocks, nb);
+    return hipGetLastError();
+}
+
+hipError_t launch_dct2d_blocks(float *blocks, int64_t nb, int block, int inverse, hipStream_t st)
+{
+    if (nb == 0) return hipSuccess;
+    switch (block) {
+    case 4: return launch_dct_b<4>(blocks, nb, inverse, st);
+    case 8: return launch_dct_b<8>(blocks, nb, inverse, st);
+    case 16: return launch_dct_b<16>(blocks, nb, inverse, st);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+template <int B>
+static hipError_t launch_svd_b(const float *D, int64_t nb, float *U, float *S, float *Vt, int32_t *sweeps, hipStream_t st)
+{
+    const unsigned grid = (unsigned)((nb + Geo<B>::BPW - 1) / Geo<B>::BPW);
+    hipLaunchKernelGGL(svd_blocks_kernel<B>, dim3(grid), dim3(64), 0, st, D, nb, U, S, Vt, sweeps);
+    return hipGetLastError();
+}
+
+hipError_t launch_svd_blocks(const float *D, int64_t nb, int block, float *U, float *S, float *Vt, int32_t *sweeps, hipStream_t st)
+{
+    if (nb == 0) return hipSuccess;
+    switch (block) {
+    case 4: return launch_svd_b<4>(D, nb, U, S, Vt, sweeps, st);
+    case 8: return launch_svd_b<8>(D, nb, U, S, Vt, sweeps, st);
+    case 16: return launch_svd_b<16>(D, nb, U, S, Vt, sweeps, st);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_synth(uint64_t seed, int64_t frame0, int64_t nframes, int64_t frame_bytes, uint8_t *out, hipStream_t st)
+{
+    if (nframes == 0 || frame_bytes == 0) return hipSuccess;
+    const int64_t per = (frame_bytes + 1023) / 1024;
+    const unsigned gx = (unsigned)(per < 4096 ? per : 4096);
+    for (int64_t f0 = 0; f0 < nframes; f0 += 65535) {
+        const int64_t nf = nframes - f0 < 65535 ? nframes - f0 : 65535;
+        hipLaunchKernelGGL(synth_kernel, dim3(gx, (unsigned)nf), dim3(256), 0, st, seed, frame0 + f0, frame_bytes, out + f0 * frame_bytes);
+    }
+    return hipGetLastError();
+}
+
+}  // namespace tmf

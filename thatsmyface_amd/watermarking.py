@@ -1,0 +1,189 @@
+"""Drop-in for ``modules/watermarking.py`` of ThatsMyFace, running on MI355X.
+
+Same module surface and signatures as the reference
+(/root/reference/modules/watermarking.py): ``get_watermark_settings`` (:10),
+``rgb_to_ycbcr`` (:23), ``ycbcr_to_rgb`` (:53), ``apply_dct_to_block`` (:76),
+``apply_idct_to_block`` (:81), ``resize_watermark`` (:86), ``embed_watermark``
+(:135), ``extract_watermark`` (:224).  The host keeps the reference's PIL
+preparation (mode conversion, watermark decode + LANCZOS resize); every
+per-pixel and per-block loop runs in libtmfwm.so's HIP kernels and returns
+the reference's bytes.  There is no CPU fallback: without the
+built library or a GPU these functions raise.
+
+Deviations: block sizes other than 4, 8, 16 raise
+NotImplementedError; an original image smaller than the watermarked one raises
+ValueError (the reference raises for a full block of shortfall and silently
+computes partial blocks for less); array inputs to the helper functions must be
+uint8 RGB(A) / float32 as the reference itself produces them.
+"""
+from __future__ import annotations
+
+import ctypes
+import io
+
+import numpy as np
+from PIL import Image
+
+from . import _lib
+from .constants import ALPHA, BLOCK_SIZE
+
+__all__ = [
+    "get_watermark_settings",
+    "rgb_to_ycbcr",
+    "ycbcr_to_rgb",
+    "apply_dct_to_block",
+    "apply_idct_to_block",
+    "resize_watermark",
+    "embed_watermark",
+    "extract_watermark",
+]
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data_as(ctypes.c_void_p).value or 0
+
+
+def get_watermark_settings():
+    """watermarking.py:10-20: session-state settings, else the module defaults.
+
+    streamlit is imported lazily (the reference imports it at module top, :5, but
+    uses it only here), so the module also works outside a Streamlit app.
+    """
+    try:
+        import streamlit as st  # noqa: PLC0415
+    except ImportError:
+        return {"block_size": BLOCK_SIZE, "alpha": ALPHA}
+    state = getattr(st, "session_state", {})
+    if "custom_settings" in state:
+        settings = state.custom_settings if hasattr(state, "custom_settings") else state["custom_settings"]
+        return {
+            "block_size": settings.get("block_size", BLOCK_SIZE),
+            "alpha": settings.get("alpha", ALPHA),
+        }
+    return {"block_size": BLOCK_SIZE, "alpha": ALPHA}
+
+
+def _as_rgb_u8(img) -> np.ndarray:
+    if isinstance(img, Image.Image):
+        img = img.convert("RGB")
+    arr = np.asarray(img)
+    if arr.ndim != 3 or arr.shape[-1] not in (3, 4):
+        raise ValueError(f"expected an (H, W, 3|4) image, got shape {arr.shape}")
+    if arr.dtype != np.uint8:
+        raise TypeError(f"expected uint8 pixels, got {arr.dtype}")
+    if arr.shape[-1] == 4:  # :32-34 RGBA -> first three channels
+        arr = arr[..., :3]
+    return np.ascontiguousarray(arr)
+
+
+def rgb_to_ycbcr(img) -> np.ndarray:
+    """watermarking.py:23-50 on the GPU: (H, W, 3) float32 (Y, Cb + 0.5, Cr + 0.5)."""
+    rgb = _as_rgb_u8(img)
+    out = np.empty(rgb.shape[:2] + (3,), np.float32)
+    L = _lib.load()
+    _lib.check(L.tmfwm_rgb_to_ycbcr(_ptr(rgb), rgb.shape[0] * rgb.shape[1], _ptr(out), _lib.MEM_HOST, None), "rgb_to_ycbcr")
+    return out
+
+
+def ycbcr_to_rgb(img) -> np.ndarray:
+    """watermarking.py:53-73 on the GPU: (H, W, 3) float32 -> (H, W, 3) uint8."""
+    ycc = np.ascontiguousarray(img, dtype=np.float32)
+    if ycc.ndim != 3 or ycc.shape[-1] != 3:
+        raise ValueError(f"expected an (H, W, 3) array, got shape {ycc.shape}")
+    out = np.empty(ycc.shape, np.uint8)
+    L = _lib.load()
+    _lib.check(L.tmfwm_ycbcr_to_rgb(_ptr(ycc), ycc.shape[0] * ycc.shape[1], _ptr(out), _lib.MEM_HOST, None), "ycbcr_to_rgb")
+    return out
+
+
+def _dct_blocks(block, inverse: bool) -> np.ndarray:
+    arr = np.asarray(block)
+    if arr.dtype != np.float32:
+        raise NotImplementedError(f"DCT blocks are float32 on this path (got {arr.dtype})")
+    if arr.ndim < 2 or arr.shape[-1] != arr.shape[-2]:
+        raise NotImplementedError(f"square b x b blocks only (got {arr.shape})")
+    out = np.array(arr, dtype=np.float32, order="C", copy=True)
+    b = out.shape[-1]
+    L = _lib.load()
+    _lib.check(L.tmfwm_dct2d_blocks(_ptr(out), out.size // (b * b), b, int(inverse), _lib.MEM_HOST, None),
+               "apply_idct_to_block" if inverse else "apply_dct_to_block")
+    return out
+
+
+def apply_dct_to_block(block) -> np.ndarray:
+    """watermarking.py:76-78: 2-D orthonormal DCT-II, axis 0 then axis 1 (also on a stack of blocks)."""
+    return _dct_blocks(block, False)
+
+
+def apply_idct_to_block(block) -> np.ndarray:
+    """watermarking.py:81-83: 2-D orthonormal DCT-III, axis 0 then axis 1."""
+    return _dct_blocks(block, True)
+
+
+def resize_watermark(watermark, target_height, target_width, preserve_ratio=False):
+    """watermarking.py:86-132, same PIL operations (host side by design)."""
+    watermark_img = Image.open(io.BytesIO(watermark)) if isinstance(watermark, bytes) else watermark
+    watermark_img = watermark_img.convert("L")
+    if preserve_ratio:
+        original_width, original_height = watermark_img.size
+        ratio = min(target_width / original_width, target_height / original_height)
+        new_width = int(original_width * ratio)
+        new_height = int(original_height * ratio)
+        resized = watermark_img.resize((new_width, new_height), Image.LANCZOS)
+        final = Image.new("L", (target_width, target_height), 255)
+        final.paste(resized, ((target_width - new_width) // 2, (target_height - new_height) // 2))
+        return final
+    return watermark_img.resize((target_width, target_height), Image.LANCZOS)
+
+
+def _settings(custom_settings):
+    settings = custom_settings if custom_settings else get_watermark_settings()
+    return settings.get("block_size", BLOCK_SIZE), settings.get("alpha", ALPHA)
+
+
+def embed_watermark(image, watermark_data, preserve_ratio=False, custom_settings=None):
+    """watermarking.py:135-221: returns a new RGB PIL image of the same size."""
+    block_size, alpha = _settings(custom_settings)
+    image = image.convert("RGB")
+    watermark_img = Image.open(io.BytesIO(watermark_data)) if isinstance(watermark_data, bytes) else watermark_data
+    rgb = np.ascontiguousarray(np.asarray(image, dtype=np.uint8))
+    height, width = rgb.shape[:2]
+    block_size = int(block_size)
+    if block_size <= 0:
+        raise ValueError(f"block_size must be positive, got {block_size}")
+    nbh, nbw = height // block_size, width // block_size
+    tile = np.ascontiguousarray(np.asarray(resize_watermark(watermark_img, nbh, nbw, preserve_ratio), dtype=np.uint8))
+    out = np.empty_like(rgb)
+    L = _lib.load()
+    _lib.check(
+        L.tmfwm_embed(_ptr(rgb), 1, height, width, rgb.size, _ptr(tile), block_size, float(alpha), _ptr(out), _lib.MEM_HOST, None),
+        "embed_watermark",
+    )
+    return Image.fromarray(out)
+
+
+def extract_watermark(watermarked_image, original_image, custom_settings=None):
+    """watermarking.py:224-294: returns the (W/b) x (H/b) mode-"L" extracted watermark."""
+    block_size, alpha = _settings(custom_settings)
+    block_size = int(block_size)
+    if block_size <= 0:
+        raise ValueError(f"block_size must be positive, got {block_size}")
+    w = np.asarray(watermarked_image.convert("RGB"), dtype=np.uint8)
+    o = np.asarray(original_image.convert("RGB"), dtype=np.uint8)
+    height, width = w.shape[:2]
+    nbh, nbw = height // block_size, width // block_size
+    if nbh == 0 or nbw == 0:
+        return Image.fromarray(np.zeros((nbh, nbw), np.uint8))
+    if o.shape[0] < height or o.shape[1] < width:
+        raise ValueError(
+            f"original image {o.shape[1]}x{o.shape[0]} is smaller than the watermarked image {width}x{height}"
+        )
+    w = np.ascontiguousarray(w)
+    o = np.ascontiguousarray(o[:height, :width])  # the reference slices the original with the watermarked grid
+    out = np.empty((nbh, nbw), np.uint8)
+    L = _lib.load()
+    _lib.check(
+        L.tmfwm_extract(_ptr(w), _ptr(o), 1, height, width, w.size, block_size, float(alpha), _ptr(out), _lib.MEM_HOST, None),
+        "extract_watermark",
+    )
+    return Image.fromarray(out)
