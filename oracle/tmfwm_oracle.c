@@ -418,29 +418,49 @@ static void jac_pairs(int b, int s, int p, int *pi, int *pj)
     *pj = a < c ? c : a;
 }
 
-/* A (b x b, row-major, f64) is overwritten with A*V; V (row-major) accumulates.  Returns sweeps done. */
+/* Rotation of pair (i,j) from alpha = |a_i|^2, beta = |a_j|^2, gamma = a_i.a_j
+ * (DESIGN.md 3.4).  With d = beta - alpha, g = 2 gamma, r = sqrt(d^2 + g^2),
+ * w = |d| + r and q = 1/sqrt(2 r w):  c = w q,  s = sgn(d) g q  (t = s/c is the
+ * small root of t^2 gamma + t d - gamma = 0), and t*gamma = sgn(d) g^2 r q^2
+ * updates the column norms: alpha' = alpha - t gamma, beta' = beta + t gamma. */
+static void rotation(double alpha, double beta, double gamma, double *c, double *s, double *tg)
+{
+    const double d = beta - alpha;
+    const double g = gamma + gamma;
+    const double r = sqrt(fma(d, d, g * g));
+    const double w = fabs(d) + r;
+    const double q = 1.0 / sqrt((r + r) * w);
+    const double sg = copysign(1.0, d);
+    *c = w * q;
+    *s = (g * sg) * q;
+    *tg = (((g * g) * r) * (q * q)) * sg;
+}
+
+/* A (b x b, row-major, f64) is overwritten with A*V; V (row-major) accumulates.
+ * Column norms are recomputed (contract dot) at the start of every sweep and
+ * updated with t*gamma inside it.  Returns sweeps done. */
 static int jacobi(double *A, double *V, int b, int want_v)
 {
     int sweep;
-    double F = 0.0;
+    double F = 0.0, nrm[ORC_MAXB];
     for (int k = 0; k < b; ++k) F += cdot(A + k, A + k, b, b);
     const double c2 = JAC_C2 * F;
     for (sweep = 0; sweep < JAC_MAX_SWEEPS; ++sweep) {
         int rotated = 0;
-        for (int s = 0; s < b - 1; ++s) {
+        for (int k = 0; k < b; ++k) nrm[k] = cdot(A + k, A + k, b, b);
+        for (int st = 0; st < b - 1; ++st) {
             for (int p = 0; p < b / 2; ++p) {
                 int i, j;
-                jac_pairs(b, s, p, &i, &j);
-                const double alpha = cdot(A + i, A + i, b, b);
-                const double beta = cdot(A + j, A + j, b, b);
+                jac_pairs(b, st, p, &i, &j);
+                const double alpha = nrm[i], beta = nrm[j];
                 const double gamma = cdot(A + i, A + j, b, b);
                 const double g2 = gamma * gamma;
                 if (g2 <= c2 * (alpha + beta) || g2 <= (JAC_TOL2 * alpha) * beta) continue;
                 rotated = 1;
-                const double zeta = (beta - alpha) / (2.0 * gamma);
-                const double t = copysign(1.0, zeta) / (fabs(zeta) + sqrt(fma(zeta, zeta, 1.0)));
-                const double c = 1.0 / sqrt(fma(t, t, 1.0));
-                const double sn = c * t;
+                double c, sn, tg;
+                rotation(alpha, beta, gamma, &c, &sn, &tg);
+                nrm[i] = alpha - tg;
+                nrm[j] = beta + tg;
                 for (int r = 0; r < b; ++r) {
                     const double x = A[r * b + i], y = A[r * b + j];
                     A[r * b + i] = fma(-sn, y, c * x);
@@ -458,8 +478,6 @@ static int jacobi(double *A, double *V, int b, int want_v)
     }
     return sweep;
 }
-
-
 
 /* Full SVD of one block: D (b x b f32 row-major) -> U (b x b), S (b), Vt (b x b), f32, sorted descending.
  * Returns number of sweeps. */

@@ -480,25 +480,46 @@ TMF_DEVI double cdot(const double (&A)[R][B], int i, int j)
 }
 
 struct Rot {
-    double c, s;
-    int on;
+    double c, s, tg;
 };
 
-TMF_DEVI Rot rotation(double alpha, double beta, double gamma, double c2)
+// Bitwise blend with an opaque lane mask: keeps the selection a v_bfi_b32 on values,
+// so the optimiser cannot turn "pick nrm[i] by lane" into a dynamically indexed
+// (scratch) array access.
+TMF_DEVI double blend_d(int mask, double x, double y)
 {
-    Rot r;
+    const long long m = (long long)mask;  // 0 or -1
+    const long long xb = __builtin_bit_cast(long long, x), yb = __builtin_bit_cast(long long, y);
+    return __builtin_bit_cast(double, (xb & m) | (yb & ~m));
+}
+
+// Rotation of a pair (oracle rotation()): 2 sqrt + 1 divide.
+TMF_DEVI Rot rotation(double alpha, double beta, double gamma)
+{
+    Rot o;
+    const double d = beta - alpha;
+    const double g = gamma + gamma;
+    const double r = __builtin_sqrt(__builtin_fma(d, d, g * g));
+    const double w = __builtin_fabs(d) + r;
+    const double q = 1.0 / __builtin_sqrt((r + r) * w);
+    const double sg = __builtin_copysign(1.0, d);
+    o.c = w * q;
+    o.s = (g * sg) * q;
+    o.tg = (((g * g) * r) * (q * q)) * sg;
+    return o;
+}
+
+TMF_DEVI bool rotate_test(double alpha, double beta, double gamma, double c2)
+{
     const double g2 = gamma * gamma;
-    r.on = !(g2 <= c2 * (alpha + beta) || g2 <= (kTol2 * alpha) * beta);
-    const double zeta = (beta - alpha) / (2.0 * gamma);
-    const double t = __builtin_copysign(1.0, zeta) / (__builtin_fabs(zeta) + __builtin_sqrt(__builtin_fma(zeta, zeta, 1.0)));
-    r.c = 1.0 / __builtin_sqrt(__builtin_fma(t, t, 1.0));
-    r.s = r.c * t;
-    return r;
+    return !(g2 <= c2 * (alpha + beta) || g2 <= (kTol2 * alpha) * beta);
 }
 
 // One-sided Jacobi on A (and V when WANT_V).  Returns sweeps executed by the wave.
-// Pairs of a round are disjoint, so they are applied in any order; lane q of a group
-// evaluates the rotations of pairs [q*PP, q*PP+PP) and broadcasts them.
+// Pairs of a round are disjoint, so they are applied in any order.  Every lane of
+// a group holds the column norms; lane q evaluates the rotations of pairs
+// [q*PP, q*PP+PP) and broadcasts (c, s, t*gamma).  Updates run under an exec
+// mask (never if-converted): lanes of blocks that skip a pair keep their bits.
 template <int B, int L, bool WANT_V>
 TMF_DEVI int jacobi(double (&A)[B / L][B], double (&V)[B / L][B], int q)
 {
@@ -509,31 +530,49 @@ TMF_DEVI int jacobi(double (&A)[B / L][B], double (&V)[B / L][B], int q)
     const double c2 = kC2 * F;
     int sweep = 0;
     for (; sweep < kMaxSweeps; ++sweep) {
+        double nrm[B];
+        static_for<B>([&](auto K) { nrm[K] = cdot<R, B, L>(A, K, K); });
         int rotated = 0;
         static_for<B - 1>([&](auto S) {
             constexpr int s = S;
-            // alpha, beta, gamma of the pairs this lane evaluates
-            double al[PP], be[PP], ga[PP];
+            double ga[NP];
+            bool on[NP];
             static_for<NP>([&](auto P) {
-                constexpr int p = P, i = Sched<B>::lo(s, p), j = Sched<B>::hi(s, p), u = p % PP;
-                const double a = cdot<R, B, L>(A, i, i);
-                const double b = cdot<R, B, L>(A, j, j);
-                const double g = cdot<R, B, L>(A, i, j);
-                if (p / PP == 0 || p / PP == q) {
-                    al[u] = a;
-                    be[u] = b;
-                    ga[u] = g;
+                constexpr int p = P, i = Sched<B>::lo(s, p), j = Sched<B>::hi(s, p);
+                ga[p] = cdot<R, B, L>(A, i, j);
+                on[p] = rotate_test(nrm[i], nrm[j], ga[p], c2);
+            });
+            // parameters of this lane's pairs
+            Rot mine[PP];
+            static_for<PP>([&](auto U) {
+                constexpr int p0 = U, i0 = Sched<B>::lo(s, p0), j0 = Sched<B>::hi(s, p0);
+                double a = nrm[i0], b = nrm[j0], g = ga[p0];
+                bool o = on[p0];
+                static_for<L - 1>([&](auto Q1) {
+                    constexpr int QQ = Q1 + 1, p = QQ * PP + U, i = Sched<B>::lo(s, p), j = Sched<B>::hi(s, p);
+                    int m = -(int)(q == QQ);
+                    asm volatile("" : "+v"(m));
+                    a = blend_d(m, nrm[i], a);
+                    b = blend_d(m, nrm[j], b);
+                    g = blend_d(m, ga[p], g);
+                    o = (m & (int)on[p]) | (~m & (int)o);
+                });
+                mine[U] = Rot{1.0, 0.0, 0.0};
+                if (o) {
+                    asm volatile("" ::: "memory");
+                    mine[U] = rotation(a, b, g);
                 }
             });
-            Rot mine[PP];
-            static_for<PP>([&](auto U) { mine[U] = rotation(al[U], be[U], ga[U], c2); });
             static_for<NP>([&](auto P) {
                 constexpr int p = P, i = Sched<B>::lo(s, p), j = Sched<B>::hi(s, p), u = p % PP, src = p / PP;
                 const double c = group_bcast<L, src>(mine[u].c);
                 const double sn = group_bcast<L, src>(mine[u].s);
-                const int on = group_bcast_i<L, src>(mine[u].on);
-                if (on) {
+                const double tg = group_bcast<L, src>(mine[u].tg);
+                if (on[p]) {
+                    asm volatile("" ::: "memory");
                     rotated = 1;
+                    nrm[i] = nrm[i] - tg;
+                    nrm[j] = nrm[j] + tg;
 #pragma unroll
                     for (int r = 0; r < R; ++r) {
                         const double x = A[r][i], y = A[r][j];

@@ -151,18 +151,25 @@ TMF_DEVI void luma_rows(const uint32_t (&words)[Geo<B>::R][Geo<B>::NW], float (&
 template <int B>
 __global__ __launch_bounds__(64) void embed_kernel(EmbedArgs a)
 {
-    constexpr int L = Geo<B>::L, R = Geo<B>::R, BPW = Geo<B>::BPW, LD = B + 1;
+    constexpr int L = Geo<B>::L, R = Geo<B>::R, BPW = Geo<B>::BPW, LD = B + 1, NW = Geo<B>::NW;
     __shared__ float lds[BPW * B * LD];
+    __shared__ uint32_t pix[R * NW][64];  // this lane's source bytes, parked during the SVD
     const int lane = threadIdx.x & 63, g = lane / L, q = lane % L;
     float *tile = lds + g * B * LD;
     const StripPos pos = strip_pos<B>(a.strips_per_row, a.nbw);
     const uint8_t *src = a.src + pos.frame * a.frame_stride;
     uint8_t *dst = a.dst + pos.frame * a.frame_stride;
 
-    uint32_t words[R][Geo<B>::NW];
-    load_block_rows<B>(src, a.W, pos, q, a.aligned, words);
     float x[R][B];
-    luma_rows<B>(words, x);
+    {
+        uint32_t words[R][NW];
+        load_block_rows<B>(src, a.W, pos, q, a.aligned, words);
+        luma_rows<B>(words, x);
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int i = 0; i < NW; ++i) pix[r * NW + i][lane] = words[r][i];
+    }
     dct2d_rows_layout<B, false>(x, tile, q);  // :192
 
     double A[R][B], V[R][B];
@@ -245,6 +252,11 @@ __global__ __launch_bounds__(64) void embed_kernel(EmbedArgs a)
 
     // :207-216 write back and ycbcr_to_rgb with this lane's original chroma
     if (pos.valid) {
+        uint32_t words[R][NW];
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int i = 0; i < NW; ++i) words[r][i] = pix[r * NW + i][lane];
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             uint32_t out[Geo<B>::NW];
