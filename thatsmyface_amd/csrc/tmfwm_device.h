@@ -451,6 +451,21 @@ TMF_DEVI double group_sum(double v)
     return v;
 }
 
+template <int CTRL>
+TMF_DEVI float dpp_f(float v)
+{
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+
+template <int L>
+TMF_DEVI float group_sum_f(float v)
+{
+    if constexpr (L >= 2) v = v + dpp_f<0xB1>(v);
+    if constexpr (L >= 4) v = v + dpp_f<0x4E>(v);
+    if constexpr (L >= 8) v = v + dpp_f<0x141>(v);
+    return v;
+}
+
 // value of lane (group base + K) for every lane of the group
 template <int L, int K>
 TMF_DEVI double group_bcast(double v)
@@ -596,6 +611,97 @@ TMF_DEVI int jacobi(double (&A)[B / L][B], double (&V)[B / L][B], int q)
         }
     }
     return sweep;
+}
+
+// ---------------------------------------------------------------------------
+// Certified f32(sigma_1) for the extract path.  An f32 power
+// iteration on D^T D gives a vector v; in f64 the Rayleigh quotient rho and the
+// residual bound the top eigenvalue of D^T D by Kato-Temple:
+//     lambda_1 in [rho, rho + |r|^2 / (2 rho - F)]      (needs 2 rho > F = |D|_F^2,
+// since lambda_2 <= F - lambda_1 <= F - rho).  Every f64 rounding is covered by
+// generous unit-roundoff margins, and the enclosure is widened by a further 2^-45
+// (relative) so that it also contains LAPACK's and the oracle's f64 sigma_1.
+// If both ends round to the same float, that float IS f32(sigma_1) of the
+// reference; otherwise the caller falls back to the exact Jacobi.
+// ---------------------------------------------------------------------------
+template <int B, int L, int ITERS>
+TMF_DEVI bool sigma1_certified(const float (&x)[B / L][B], float &s1)
+{
+    constexpr int R = B / L;
+    constexpr double u = 1.1102230246251565e-16;  // 2^-53
+    float v[B];
+#pragma unroll
+    for (int j = 0; j < B; ++j) v[j] = j == 0 ? 1.0f : 0.0f;
+#pragma unroll
+    for (int it = 0; it < ITERS; ++it) {
+        float uu[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            float acc = 0.0f;
+#pragma unroll
+            for (int j = 0; j < B; ++j) acc = __builtin_fmaf(x[r][j], v[j], acc);
+            uu[r] = acc;
+        }
+        float w[B], nn = 0.0f;
+#pragma unroll
+        for (int j = 0; j < B; ++j) {
+            float acc = 0.0f;
+#pragma unroll
+            for (int r = 0; r < R; ++r) acc = __builtin_fmaf(x[r][j], uu[r], acc);
+            w[j] = group_sum_f<L>(acc);
+            nn = __builtin_fmaf(w[j], w[j], nn);
+        }
+        const bool live = nn > 1e-30f;
+        const float inv = __builtin_amdgcn_rsqf(live ? nn : 1.0f);
+#pragma unroll
+        for (int j = 0; j < B; ++j) v[j] = live ? w[j] * inv : v[j];
+    }
+    double Fp = 0.0;
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int j = 0; j < B; ++j) Fp = __builtin_fma((double)x[r][j], (double)x[r][j], Fp);
+    const double F = group_sum<L>(Fp);
+    if (F == 0.0) {
+        s1 = 0.0f;
+        return true;
+    }
+    double vd[B], nv = 0.0;
+#pragma unroll
+    for (int j = 0; j < B; ++j) {
+        vd[j] = (double)v[j];
+        nv = __builtin_fma(vd[j], vd[j], nv);
+    }
+    double ud[R], ap = 0.0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        double acc = 0.0;
+#pragma unroll
+        for (int j = 0; j < B; ++j) acc = __builtin_fma((double)x[r][j], vd[j], acc);
+        ud[r] = acc;
+        ap = __builtin_fma(acc, acc, ap);
+    }
+    const double a = group_sum<L>(ap);
+    const double rho = a / nv;
+    double rn2 = 0.0;
+#pragma unroll
+    for (int j = 0; j < B; ++j) {
+        double acc = 0.0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc = __builtin_fma((double)x[r][j], ud[r], acc);
+        const double rj = group_sum<L>(acc) - rho * vd[j];
+        rn2 = __builtin_fma(rj, rj, rn2);
+    }
+    const double rr0 = __builtin_sqrt(rn2 / nv) * (1.0 + 16.0 * u) + 256.0 * u * F;
+    const double rr = rr0 * rr0;
+    const double rlo = rho * (1.0 - 256.0 * u);
+    const double fhi = F * (1.0 + 256.0 * u);
+    const double gap = (rlo + rlo) - fhi;
+    const double hi = (rho + rr / (gap > 0.0 ? gap : 1.0)) * (1.0 + 256.0 * u);
+    const double slo = __builtin_sqrt(rlo) * (1.0 - 512.0 * u);
+    const double shi = __builtin_sqrt(hi) * (1.0 + 512.0 * u);
+    s1 = (float)slo;
+    return gap > 0.0 && (float)shi == s1 && rho == rho;
 }
 
 }  // namespace tmf

@@ -282,8 +282,10 @@ __global__ __launch_bounds__(64) void embed_kernel(EmbedArgs a)
 // ---------------------------------------------------------------------------
 // Extract: watermarking.py:241-289 fused; sigma_1 of both images per block.
 // ---------------------------------------------------------------------------
+constexpr int kPowerIters = 6;  // f32 power iterations before certification
+
 template <int B>
-TMF_DEVI double sigma1_of(const uint8_t *frame_base, int W, const StripPos &pos, int q, bool aligned, float *tile)
+TMF_DEVI float sigma1_of(const uint8_t *frame_base, int W, const StripPos &pos, int q, bool aligned, float *tile)
 {
     constexpr int L = Geo<B>::L, R = Geo<B>::R;
     uint32_t words[R][Geo<B>::NW];
@@ -291,19 +293,26 @@ TMF_DEVI double sigma1_of(const uint8_t *frame_base, int W, const StripPos &pos,
     float x[R][B];
     luma_rows<B>(words, x);
     dct2d_rows_layout<B, false>(x, tile, q);
-    double A[R][B], V[R][B];
+    float s1;
+    const bool ok = sigma1_certified<B, L, kPowerIters>(x, s1);
+    if (!__all(ok)) {
+        // exact path (the oracle's Jacobi) for the blocks the enclosure could not decide;
+        // certified blocks enter as zero matrices and leave the sweeps at once
+        double A[R][B], V[R][B];
 #pragma unroll
-    for (int r = 0; r < R; ++r)
+        for (int r = 0; r < R; ++r)
 #pragma unroll
-        for (int c = 0; c < B; ++c) A[r][c] = (double)x[r][c];
-    jacobi<B, L, false>(A, V, q);
-    double m = 0.0;
+            for (int c = 0; c < B; ++c) A[r][c] = ok ? 0.0 : (double)x[r][c];
+        jacobi<B, L, false>(A, V, q);
+        double m = 0.0;
 #pragma unroll
-    for (int k = 0; k < B; ++k) {
-        const double s = __builtin_sqrt(cdot<R, B, L>(A, k, k));
-        m = s > m ? s : m;
+        for (int k = 0; k < B; ++k) {
+            const double s = __builtin_sqrt(cdot<R, B, L>(A, k, k));
+            m = s > m ? s : m;
+        }
+        if (!ok) s1 = (float)m;
     }
-    return m;
+    return s1;
 }
 
 template <int B>
@@ -314,8 +323,8 @@ __global__ __launch_bounds__(64) void extract_kernel(ExtractArgs a)
     const int lane = threadIdx.x & 63, g = lane / L, q = lane % L;
     float *tile = lds + g * B * LD;
     const StripPos pos = strip_pos<B>(a.strips_per_row, a.nbw);
-    const float sw = (float)sigma1_of<B>(a.wsrc + pos.frame * a.frame_stride, a.W, pos, q, a.aligned, tile);
-    const float so = (float)sigma1_of<B>(a.osrc + pos.frame * a.frame_stride, a.W, pos, q, a.aligned, tile);
+    const float sw = sigma1_of<B>(a.wsrc + pos.frame * a.frame_stride, a.W, pos, q, a.aligned, tile);
+    const float so = sigma1_of<B>(a.osrc + pos.frame * a.frame_stride, a.W, pos, q, a.aligned, tile);
     // :285 under numpy-2 NEP 50: (f32 - f32) / f32(alpha) in f32; :288-289 clip, *255 in f64, trunc
     const float e = (sw - so) / a.alpha32;
     double d = (double)e;
