@@ -83,50 +83,45 @@ def main():
     torch.cuda.set_device(dev)
 
     from thatsmyface_amd import batch
+    from thatsmyface_amd.dist import ShardedRoundTrip, max_over_ranks, shard_range
 
     F, H, W, b, alpha = args.frames, args.height, args.width, args.block, args.alpha
     nbh, nbw = H // b, W // b
-    frames = batch.synth_frames(F, H, W, seed=batch.SEED_COVER, frame0=rank * F, device=dev)
-    out = torch.empty_like(frames)
-    tiles = torch.empty((F, nbh, nbw), dtype=torch.uint8, device=dev)
-    wm = batch.synth_tile(nbh, nbw, device=dev) if rank == 0 else torch.empty((nbh, nbw), dtype=torch.uint8, device=dev)
+    start, stop = shard_range(F * world, rank, world)  # weak scaling: F frames per GPU
+    frames = batch.synth_frames(stop - start, H, W, seed=batch.SEED_COVER, frame0=start, device=dev)
+    wm = batch.synth_tile(nbh, nbw, device=dev) if rank == 0 else torch.zeros((nbh, nbw), dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
 
     stream = torch.cuda.current_stream()
-    ev = []
+    marks = {}
 
-    def step(timed: bool):
-        if world > 1:
-            dist.broadcast(wm, src=0)  # RCCL over xGMI: the app's tile reaches every GPU
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        e2 = torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        batch.embed_batch(frames, wm, b, alpha, out=out)
-        e1.record(stream)
-        batch.extract_batch(out, frames, b, alpha, out=tiles)
-        e2.record(stream)
-        if timed:
-            ev.append((e0, e1, e2))
+    def hook(phase):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record(stream)
+        marks.setdefault(phase, []).append(e)
+
+    rt = ShardedRoundTrip(
+        embed_fn=lambda f, t, bb, a, o: batch.embed_batch(f, t, bb, a, out=o),
+        extract_fn=lambda w_, o_, bb, a, out: batch.extract_batch(w_, o_, bb, a, out=out),
+        frames=frames, tile=wm, block=b, alpha=alpha,
+    )
 
     for _ in range(args.warmup):
-        step(False)
+        rt.step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    rt.hooks.append(hook)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step(True)
+        rt.step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(time.perf_counter() - t0, dev)
+    ev = list(zip(marks["broadcast"], marks["embed"], marks["extract"]))
 
     embed_ms = sum(a.elapsed_time(m) for a, m, _ in ev) / len(ev)
     extract_ms = sum(m.elapsed_time(z) for _, m, z in ev) / len(ev)

@@ -1,0 +1,83 @@
+"""CPU checks of the C-ABI boundary: libtmfwm.so loads, exports exactly what
+include/tmfwm.h declares, validates arguments, and fails loudly without a GPU
+(no CPU fallback).  No compute runs here."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from thatsmyface_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    with open(os.path.join(ROOT, "include", "tmfwm.h")) as f:
+        text = f.read()
+    return sorted(set(re.findall(r"\b(tmfwm_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_library_exports_every_header_symbol():
+    L = _lib.load()
+    names = header_functions()
+    assert len(names) >= 10
+    for n in names:
+        assert hasattr(L, n), n
+    assert set(names) == set(_lib.SIGNATURES), "ctypes signatures out of sync with include/tmfwm.h"
+
+
+def test_nm_exports_match_header():
+    import subprocess
+
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    exported = sorted(set(re.findall(r" T (tmfwm_[a-z0-9_]+)", out)))
+    assert exported == header_functions()
+
+
+def test_abi_version_and_device_count():
+    L = _lib.load()
+    assert L.tmfwm_abi_version() == _lib.ABI_VERSION == 1
+    assert _lib.device_count() >= 0
+
+
+def test_argument_validation_before_device():
+    L = _lib.load()
+    a = np.zeros((16, 16, 3), np.uint8)
+    t = np.zeros((2, 2), np.uint8)
+    o = np.empty_like(a)
+    p = lambda x: x.ctypes.data  # noqa: E731
+    with pytest.raises(NotImplementedError):  # block 6 (UI slider value) is not supported
+        _lib.check(L.tmfwm_embed(p(a), 1, 16, 16, a.size, p(t), 6, 0.1, p(o), _lib.MEM_HOST, None), "embed")
+    with pytest.raises(ValueError):  # negative size
+        _lib.check(L.tmfwm_embed(p(a), -1, 16, 16, a.size, p(t), 8, 0.1, p(o), _lib.MEM_HOST, None), "embed")
+    with pytest.raises(ValueError):  # frame stride shorter than a frame
+        _lib.check(L.tmfwm_embed(p(a), 2, 16, 16, 10, p(t), 8, 0.1, p(o), _lib.MEM_HOST, None), "embed")
+    with pytest.raises(ValueError):  # alpha NaN
+        _lib.check(L.tmfwm_embed(p(a), 1, 16, 16, a.size, p(t), 8, float("nan"), p(o), _lib.MEM_HOST, None), "embed")
+    assert "frame_stride" in _lib.last_error() or "alpha" in _lib.last_error()
+
+
+@pytest.mark.skipif(_lib.device_count() > 0, reason="CPU-only check")
+def test_fails_loudly_without_gpu():
+    from thatsmyface_amd import watermarking as W
+
+    with pytest.raises(_lib.TmfwmError, match="no HIP device"):
+        W.rgb_to_ycbcr(np.zeros((4, 4, 3), np.uint8))
+    from PIL import Image
+
+    with pytest.raises(_lib.TmfwmError):
+        W.embed_watermark(Image.new("RGB", (16, 16)), Image.new("L", (2, 2)), False, {"block_size": 8, "alpha": 0.1})
+
+
+def test_product_never_imports_oracle():
+    pkg = os.path.join(ROOT, "thatsmyface_amd")
+    for dp, _, fs in os.walk(pkg):
+        for f in fs:
+            if f.endswith((".py", ".cpp", ".hip", ".h")):
+                with open(os.path.join(dp, f)) as fh:
+                    src = fh.read()
+                assert not re.search(r"^\s*(from|import)\s+oracle\b", src, re.M), f
+                assert "tmfwm_oracle" not in src, f
+                assert "libtmfwm_oracle" not in src, f

@@ -1,0 +1,81 @@
+"""Host-side logic of the drop-in module (no GPU): settings resolution
+(watermarking.py:10-20), watermark resize (:86-132) against the reference's
+tiles, and the argument checks that run before any kernel."""
+import io
+import sys
+import types
+
+import numpy as np
+import pytest
+from PIL import Image
+
+from thatsmyface_amd import watermarking as W
+
+
+def test_settings_defaults_without_streamlit(monkeypatch):
+    monkeypatch.setitem(sys.modules, "streamlit", None)  # import fails -> defaults
+    assert W.get_watermark_settings() == {"block_size": 8, "alpha": 0.1}
+
+
+def test_settings_from_session_state(monkeypatch):
+    class State(dict):
+        def __getattr__(self, k):
+            return self[k]
+
+    st = types.ModuleType("streamlit")
+    st.session_state = State(custom_settings={"block_size": 16})
+    monkeypatch.setitem(sys.modules, "streamlit", st)
+    assert W.get_watermark_settings() == {"block_size": 16, "alpha": 0.1}
+    st.session_state = State()
+    assert W.get_watermark_settings() == {"block_size": 8, "alpha": 0.1}
+
+
+def test_resize_watermark_matches_reference_tiles(golden):
+    cases, meta = golden
+    for name, m in meta["cases"].items():
+        wm = cases[f"{name}/wm"]
+        b = m["block"]
+        cov = cases[f"{name}/cover"]
+        nbh, nbw = cov.shape[0] // b, cov.shape[1] // b
+        src = Image.fromarray(wm, "L")
+        if m["wm_as_png_bytes"]:
+            buf = io.BytesIO()
+            src.save(buf, format="PNG")
+            src = buf.getvalue()
+        tile = W.resize_watermark(src, nbh, nbw, m["preserve_ratio"])
+        assert tile.mode == "L"
+        assert np.array_equal(np.asarray(tile), cases[f"{name}/tile"]), name
+
+
+def test_extract_rejects_smaller_original():
+    big = Image.new("RGB", (64, 64))
+    with pytest.raises(ValueError, match="smaller"):
+        W.extract_watermark(big, Image.new("RGB", (56, 64)), {"block_size": 8, "alpha": 0.1})
+
+
+def test_extract_tiny_image_is_empty_like_reference():
+    img = Image.new("RGB", (5, 5))
+    out = W.extract_watermark(img, img, {"block_size": 8, "alpha": 0.1})
+    assert np.asarray(out).shape == (0, 0)
+
+
+def test_embed_tiny_image_raises_like_reference():
+    # the reference's PIL resize raises "height and width must be > 0"
+    with pytest.raises(ValueError):
+        W.embed_watermark(Image.new("RGB", (5, 5)), Image.new("L", (4, 4)), False, {"block_size": 8, "alpha": 0.1})
+
+
+def test_helper_input_checks():
+    with pytest.raises(TypeError):
+        W.rgb_to_ycbcr(np.zeros((2, 2, 3), np.float32))
+    with pytest.raises(NotImplementedError):
+        W.apply_dct_to_block(np.zeros((8, 8), np.float64))
+    with pytest.raises(NotImplementedError):
+        W.apply_dct_to_block(np.zeros((8, 4), np.float32))
+
+
+def test_module_path_shim():
+    from thatsmyface_amd.modules import constants, watermarking
+
+    assert watermarking.embed_watermark is W.embed_watermark
+    assert constants.BLOCK_SIZE == 8 and constants.ALPHA == 0.1

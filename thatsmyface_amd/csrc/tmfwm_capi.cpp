@@ -79,6 +79,12 @@ int check_frames(int64_t n, int32_t H, int32_t W, int64_t stride, int32_t block)
     if (n < 0 || H < 0 || W < 0) return fail(TMFWM_ERR_INVALID, "negative size (n=%lld, H=%d, W=%d)", (long long)n, H, W);
     if (!supported_block(block)) return fail(TMFWM_ERR_UNSUPPORTED, "block size %d not supported (4, 8, 16)", block);
     if (stride < (int64_t)H * W * 3) return fail(TMFWM_ERR_INVALID, "frame_stride %lld < H*W*3", (long long)stride);
+    return 0;
+}
+
+// After argument validation: there is no CPU fallback, so no device is an error.
+int need_device()
+{
     int dev = 0;
     if (hipGetDeviceCount(&dev) != hipSuccess || dev == 0) {
         (void)hipGetLastError();
@@ -113,6 +119,7 @@ int tmfwm_embed(const uint8_t *rgb, int64_t n_frames, int32_t height, int32_t wi
     t_err.clear();
     if (int rc = check_frames(n_frames, height, width, frame_stride, block)) return rc;
     if (!std::isfinite(alpha)) return fail(TMFWM_ERR_INVALID, "alpha is not finite");
+    if (int rc = need_device()) return rc;
     if (n_frames == 0 || height == 0 || width == 0) return 0;
     const int nbh = height / block, nbw = width / block;
     const int64_t fbytes = (int64_t)height * width * 3;
@@ -171,6 +178,7 @@ int tmfwm_extract(const uint8_t *wm_rgb, const uint8_t *orig_rgb, int64_t n_fram
     t_err.clear();
     if (int rc = check_frames(n_frames, height, width, frame_stride, block)) return rc;
     if (!std::isfinite(alpha) || alpha == 0.0) return fail(TMFWM_ERR_INVALID, "alpha must be finite and non-zero");
+    if (int rc = need_device()) return rc;
     const int nbh = height / block, nbw = width / block;
     const int64_t tbytes = (int64_t)nbh * nbw;
     if (n_frames == 0 || tbytes == 0) return 0;
@@ -221,7 +229,7 @@ int tmfwm_rgb_to_ycbcr(const uint8_t *rgb, int64_t npix, float *ycc, int32_t mem
     t_err.clear();
     if (npix < 0) return fail(TMFWM_ERR_INVALID, "npix < 0");
     if (npix == 0) return 0;
-    if (int rc = check_frames(0, 0, 0, 0, 8)) return rc;
+    if (int rc = need_device()) return rc;
     hipStream_t st = pick_stream(hip_stream);
     if (mem_kind == TMFWM_MEM_DEVICE) {
         if (int rc = check_device_ptr(rgb, "rgb")) return rc;
@@ -245,7 +253,7 @@ int tmfwm_ycbcr_to_rgb(const float *ycc, int64_t npix, uint8_t *rgb, int32_t mem
     t_err.clear();
     if (npix < 0) return fail(TMFWM_ERR_INVALID, "npix < 0");
     if (npix == 0) return 0;
-    if (int rc = check_frames(0, 0, 0, 0, 8)) return rc;
+    if (int rc = need_device()) return rc;
     hipStream_t st = pick_stream(hip_stream);
     if (mem_kind == TMFWM_MEM_DEVICE) {
         if (int rc = check_device_ptr(ycc, "ycc")) return rc;
@@ -269,6 +277,7 @@ int tmfwm_dct2d_blocks(float *blocks, int64_t n_blocks, int32_t block, int32_t i
     t_err.clear();
     if (n_blocks < 0) return fail(TMFWM_ERR_INVALID, "n_blocks < 0");
     if (int rc = check_frames(0, 0, 0, 0, block)) return rc;
+    if (int rc = need_device()) return rc;
     if (n_blocks == 0) return 0;
     hipStream_t st = pick_stream(hip_stream);
     const size_t bytes = (size_t)n_blocks * block * block * sizeof(float);
@@ -293,6 +302,7 @@ int tmfwm_svd_blocks(const float *D, int64_t n_blocks, int32_t block, float *U, 
     t_err.clear();
     if (n_blocks < 0) return fail(TMFWM_ERR_INVALID, "n_blocks < 0");
     if (int rc = check_frames(0, 0, 0, 0, block)) return rc;
+    if (int rc = need_device()) return rc;
     if (n_blocks == 0) return 0;
     hipStream_t st = pick_stream(hip_stream);
     const size_t mb = (size_t)n_blocks * block * block * sizeof(float), sb = (size_t)n_blocks * block * sizeof(float);
@@ -328,6 +338,7 @@ int tmfwm_synth_frames(uint64_t seed, int64_t frame0, int64_t n_frames, int64_t 
     t_err.clear();
     if (n_frames < 0 || frame_bytes < 0 || frame0 < 0) return fail(TMFWM_ERR_INVALID, "negative size");
     if (n_frames == 0 || frame_bytes == 0) return 0;
+    if (int rc = need_device()) return rc;
     if (int rc = check_device_ptr(out, "out")) return rc;
     TMF_HIP(tmf::launch_synth(seed, frame0, n_frames, frame_bytes, out, pick_stream(hip_stream)));
     return 0;
