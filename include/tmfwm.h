@@ -89,7 +89,8 @@ int tmfwm_dct2d_blocks(float *blocks, int64_t n_blocks, int32_t block, int32_t i
 
 /* np.linalg.svd(D) as the reference consumes it (watermarking.py:195): U, S
  * (descending), Vt in float32 for n_blocks blocks.  sweeps (optional, may be
- * NULL) receives the Jacobi sweeps executed per block. */
+ * NULL) receives the Jacobi sweeps per block: f64 sweeps | (f32 sweeps << 8)
+ * (0 for an all-zero block). */
 int tmfwm_svd_blocks(const float *D, int64_t n_blocks, int32_t block, float *U, float *S, float *Vt, int32_t *sweeps,
                      int32_t mem_kind, void *hip_stream);
 

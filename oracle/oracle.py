@@ -46,6 +46,7 @@ def lib():
             "orc_svd_blocks": (I32, [_f32p, I64, I32, _f32p, _f32p, _f32p, _i32p]),
             "orc_sigma1_block": (ctypes.c_float, [_f32p, I32]),
             "orc_blend_reconstruct": (None, [_f32p, _f32p, _f32p, I32, ctypes.c_uint8, D, _f32p]),
+            "orc_blend_reconstruct_blocks": (None, [_f32p, _f32p, _f32p, I64, I32, _u8p, D, _f32p]),
             "orc_gather_blocks": (None, [_f32p, I32, I32, I32, _f32p]),
             "orc_scatter_blocks": (None, [_f32p, I32, I32, I32, _f32p]),
             "orc_embed_frame": (I32, [_u8p, I32, I32, _u8p, I32, D, _u8p, I32]),
@@ -118,6 +119,20 @@ def svd_blocks(D: np.ndarray):
 def sigma1(D: np.ndarray) -> float:
     D = np.ascontiguousarray(D, dtype=np.float32)
     return float(lib().orc_sigma1_block(_p(D, _f32p), D.shape[-1]))
+
+
+def blend_reconstruct_blocks(U, S, Vt, w: np.ndarray, alpha: float) -> np.ndarray:
+    """N7 + N8 over nb blocks; w holds one watermark byte per block."""
+    U = np.ascontiguousarray(U, np.float32)
+    S = np.ascontiguousarray(S, np.float32)
+    Vt = np.ascontiguousarray(Vt, np.float32)
+    w = np.ascontiguousarray(w, np.uint8)
+    b = U.shape[-1]
+    nb = U.size // (b * b)
+    assert w.size == nb and S.size == nb * b and Vt.shape == U.shape
+    M = np.empty_like(U)
+    lib().orc_blend_reconstruct_blocks(_p(U, _f32p), _p(S, _f32p), _p(Vt, _f32p), nb, b, _p(w, _u8p), float(alpha), _p(M, _f32p))
+    return M
 
 
 def blend_reconstruct(U, S, Vt, w: int, alpha: float) -> np.ndarray:

@@ -418,22 +418,172 @@ static void jac_pairs(int b, int s, int p, int *pi, int *pj)
     *pj = a < c ? c : a;
 }
 
+/* 1/sqrt(x) for normal x > 0 from IEEE operations only: integer seed
+ * (0x5fe6eb50c7b537a9 - bits/2, relative error <= 3.5%) and four Newton steps
+ * y <- y * (1.5 - (x/2) y^2), each as t = y*y; u = fma(-x/2, t, 1.5); y = y*u
+ * (error 3.5e-2 -> 1.8e-3 -> 4.6e-6 -> 3e-11 -> rounding level).  Unlike the
+ * hardware v_rsq_f64 (not correctly rounded, not specified to the bit) every
+ * step is reproducible in C and on the GPU.  DESIGN.md 3.4. */
+static double rsqrt_n(double x)
+{
+    uint64_t i;
+    double y;
+    memcpy(&i, &x, 8);
+    i = 0x5fe6eb50c7b537a9ull - (i >> 1);
+    memcpy(&y, &i, 8);
+    const double hx = 0.5 * x;
+    for (int k = 0; k < 4; ++k) {
+        const double t = y * y;
+        const double u = fma(-hx, t, 1.5);
+        y = y * u;
+    }
+    return y;
+}
+
+/* f32 twin: seed 0x5f375a86, three Newton steps (f32 phase only) */
+static float rsqrtf_n(float x)
+{
+    uint32_t i;
+    float y;
+    memcpy(&i, &x, 4);
+    i = 0x5f375a86u - (i >> 1);
+    memcpy(&y, &i, 4);
+    const float hx = 0.5f * x;
+    for (int k = 0; k < 3; ++k) {
+        const float t = y * y;
+        const float u = fmaf(-hx, t, 1.5f);
+        y = y * u;
+    }
+    return y;
+}
+
 /* Rotation of pair (i,j) from alpha = |a_i|^2, beta = |a_j|^2, gamma = a_i.a_j
- * (DESIGN.md 3.4).  With d = beta - alpha, g = 2 gamma, r = sqrt(d^2 + g^2),
- * w = |d| + r and q = 1/sqrt(2 r w):  c = w q,  s = sgn(d) g q  (t = s/c is the
- * small root of t^2 gamma + t d - gamma = 0), and t*gamma = sgn(d) g^2 r q^2
- * updates the column norms: alpha' = alpha - t gamma, beta' = beta + t gamma. */
+ * (DESIGN.md 3.4).  With d = beta - alpha, g = 2 gamma, x = d^2 + g^2,
+ * r = x rsqrt(x) (= sqrt x), w = |d| + r and q = rsqrt(2 r w):  c = w q,
+ * s = sgn(d) g q (t = s/c is the small root of t^2 gamma + t d - gamma = 0), and
+ * t*gamma = sgn(d) g^2 r q^2 updates the column norms: alpha' = alpha - t gamma,
+ * beta' = beta + t gamma.  c^2 + s^2 = (w^2 + g^2)/(2 r w) = 1 exactly in real
+ * arithmetic, whatever the rounding of r. */
 static void rotation(double alpha, double beta, double gamma, double *c, double *s, double *tg)
 {
     const double d = beta - alpha;
     const double g = gamma + gamma;
-    const double r = sqrt(fma(d, d, g * g));
+    const double x = fma(d, d, g * g);
+    const double r = x * rsqrt_n(x);
     const double w = fabs(d) + r;
-    const double q = 1.0 / sqrt((r + r) * w);
+    const double q = rsqrt_n((r + r) * w);
     const double sg = copysign(1.0, d);
     *c = w * q;
     *s = (g * sg) * q;
     *tg = (((g * g) * r) * (q * q)) * sg;
+}
+
+static void rotationf(float alpha, float beta, float gamma, float *c, float *s, float *tg)
+{
+    const float d = beta - alpha;
+    const float g = gamma + gamma;
+    const float x = fmaf(d, d, g * g);
+    const float r = x * rsqrtf_n(x);
+    const float w = fabsf(d) + r;
+    const float q = rsqrtf_n((r + r) * w);
+    const float sg = copysignf(1.0f, d);
+    *c = w * q;
+    *s = (g * sg) * q;
+    *tg = (((g * g) * r) * (q * q)) * sg;
+}
+
+static float tree_sumf(float *v, int n)
+{
+    while (n > 1) {
+        for (int k = 0; k < n / 2; ++k) v[k] = v[2 * k] + v[2 * k + 1];
+        n /= 2;
+    }
+    return v[0];
+}
+
+/* f32 twin of cdot() (same chunks, fmaf chains, pairwise tree) */
+static float cdotf(const float *x, const float *y, int ld, int b)
+{
+    const int P = jac_chunks(b), R = b / P;
+    float part[ORC_MAXB];
+    for (int q = 0; q < P; ++q) {
+        float acc = 0.0f;
+        for (int r = q * R; r < (q + 1) * R; ++r) acc = fmaf(x[r * ld], y[r * ld], acc);
+        part[q] = acc;
+    }
+    return tree_sumf(part, P);
+}
+
+/* Phase 1 of the SVD: at most JAC32_MAX_SWEEPS one-sided Jacobi
+ * sweeps in f32 on A32 = D, accumulating V32 (a preconditioner: its V only has to
+ * be close to the right singular vectors; phase 3 makes them f64-accurate).
+ * Rotate iff gamma^2 > 2^-48 F^2 (gamma above the f32 noise of the whole block),
+ * gamma^2 > 2^-45 F (alpha+beta) and gamma^2 > 2^-40 alpha beta.  Blocks with
+ * F < 2^-30 skip the phase (V32 = I), which keeps every square in the normal range. */
+#define JAC32_MAX_SWEEPS 4
+#define JAC32_TOL2 9.094947017729282e-13f /* 2^-40 */
+#define JAC32_C2 2.842170943040401e-14f   /* 2^-45 */
+#define JAC32_C2A 3.552713678800501e-15f  /* 2^-48 */
+#define JAC32_FMIN 9.313225746154785e-10f /* 2^-30 */
+static int jacobi_f32(float *A, float *V, int b)
+{
+    int sweep;
+    float F = 0.0f, nrm[ORC_MAXB];
+    for (int k = 0; k < b; ++k) F += cdotf(A + k, A + k, b, b);
+    if (!(F >= JAC32_FMIN)) return 0;
+    const float c2 = JAC32_C2 * F, c2a = JAC32_C2A * (F * F);
+    for (sweep = 0; sweep < JAC32_MAX_SWEEPS; ++sweep) {
+        int rotated = 0;
+        for (int k = 0; k < b; ++k) nrm[k] = cdotf(A + k, A + k, b, b);
+        for (int st = 0; st < b - 1; ++st)
+            for (int p = 0; p < b / 2; ++p) {
+                int i, j;
+                jac_pairs(b, st, p, &i, &j);
+                const float alpha = nrm[i], beta = nrm[j];
+                const float gamma = cdotf(A + i, A + j, b, b);
+                const float g2 = gamma * gamma;
+                if (g2 <= c2a || g2 <= c2 * (alpha + beta) || g2 <= (JAC32_TOL2 * alpha) * beta) continue;
+                rotated = 1;
+                float c, sn, tg;
+                rotationf(alpha, beta, gamma, &c, &sn, &tg);
+                nrm[i] = alpha - tg;
+                nrm[j] = beta + tg;
+                for (int r = 0; r < b; ++r) {
+                    const float x = A[r * b + i], y = A[r * b + j];
+                    A[r * b + i] = fmaf(-sn, y, c * x);
+                    A[r * b + j] = fmaf(sn, x, c * y);
+                }
+                for (int r = 0; r < b; ++r) {
+                    const float x = V[r * b + i], y = V[r * b + j];
+                    V[r * b + i] = fmaf(-sn, y, c * x);
+                    V[r * b + j] = fmaf(sn, x, c * y);
+                }
+            }
+        if (!rotated) { ++sweep; break; }
+    }
+    return sweep;
+}
+
+/* Phase 2: one Bjorck / Newton-Schulz step toward the orthogonal
+ * polar factor, V <- V N with N = 1.5 I - 0.5 V^T V.  (V^T V)_jk is cdot() over
+ * rows; N_kk = fma(-0.5, Q_kk, 1.5), N_jk = -0.5 Q_jk; (V N)_rk is an fma chain
+ * over j = 0..b-1.  Two steps take the f32 phase's ~1e-6 to rounding level. */
+#define JAC_BJORCK_STEPS 2
+static void bjorck(double *V, int b)
+{
+    double N[ORC_MAXB * ORC_MAXB], T[ORC_MAXB * ORC_MAXB];
+    for (int j = 0; j < b; ++j)
+        for (int k = j; k < b; ++k) {
+            const double q = cdot(V + j, V + k, b, b);
+            N[j * b + k] = N[k * b + j] = (j == k) ? fma(-0.5, q, 1.5) : -0.5 * q;
+        }
+    for (int r = 0; r < b; ++r)
+        for (int k = 0; k < b; ++k) {
+            double acc = 0.0;
+            for (int j = 0; j < b; ++j) acc = fma(V[r * b + j], N[j * b + k], acc);
+            T[r * b + k] = acc;
+        }
+    memcpy(V, T, sizeof(double) * b * b);
 }
 
 /* A (b x b, row-major, f64) is overwritten with A*V; V (row-major) accumulates.
@@ -480,7 +630,7 @@ static int jacobi(double *A, double *V, int b, int want_v)
 }
 
 /* Full SVD of one block: D (b x b f32 row-major) -> U (b x b), S (b), Vt (b x b), f32, sorted descending.
- * Returns number of sweeps. */
+ * Returns the sweeps done: f64 sweeps | (f32 sweeps << 8). */
 int orc_svd_block(const float *D, int b, float *U, float *S, float *Vt)
 {
     double A[ORC_MAXB * ORC_MAXB], V[ORC_MAXB * ORC_MAXB], sig[ORC_MAXB];
@@ -493,7 +643,20 @@ int orc_svd_block(const float *D, int b, float *U, float *S, float *Vt)
         for (int k = 0; k < b; ++k) S[k] = 0.0f;
         return 0;
     }
-    int sweeps = jacobi(A, V, b, 1);
+    /* phase 1: f32 Jacobi on D; phase 2: V0 = Bjorck^2(f64(V32)); phase 3: f64
+     * Jacobi on A0 = D V0 (fma chain over j), accumulating onto V0 */
+    float A32[ORC_MAXB * ORC_MAXB], V32[ORC_MAXB * ORC_MAXB];
+    for (int k = 0; k < b * b; ++k) { A32[k] = D[k]; V32[k] = (k / b == k % b) ? 1.0f : 0.0f; }
+    const int s32 = jacobi_f32(A32, V32, b);
+    for (int k = 0; k < b * b; ++k) V[k] = V32[k];
+    for (int it = 0; it < JAC_BJORCK_STEPS; ++it) bjorck(V, b);
+    for (int r = 0; r < b; ++r)
+        for (int k = 0; k < b; ++k) {
+            double acc = 0.0;
+            for (int j = 0; j < b; ++j) acc = fma((double)D[r * b + j], V[j * b + k], acc);
+            A[r * b + k] = acc;
+        }
+    const int sweeps = jacobi(A, V, b, 1) | (s32 << 8);
     float Uf[ORC_MAXB * ORC_MAXB], Vf[ORC_MAXB * ORC_MAXB];
     for (int k = 0; k < b; ++k) {
         sig[k] = sqrt(cdot(A + k, A + k, b, b));
@@ -549,6 +712,12 @@ void orc_blend_reconstruct(const float *U, const float *S, const float *Vt, int 
             for (int k = 0; k < b; ++k) acc = fmaf(U[i * b + k], B[k * b + j], acc);
             M[i * b + j] = acc;
         }
+}
+
+void orc_blend_reconstruct_blocks(const float *U, const float *S, const float *Vt, int64_t nb, int b, const uint8_t *w, double alpha, float *M)
+{
+    for (int64_t k = 0; k < nb; ++k)
+        orc_blend_reconstruct(U + k * b * b, S + k * b, Vt + k * b * b, b, w[k], alpha, M + k * b * b);
 }
 
 /* ------------------------------------------------------------------------ */

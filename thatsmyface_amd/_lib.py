@@ -7,11 +7,13 @@ CPU fallback: if the library or a GPU is missing every call raises.
 from __future__ import annotations
 
 import ctypes
+import importlib.util
 import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libtmfwm.so")
+# TMFWM_LIB selects an alternative build (e.g. the phase-profile libtmfwm_stamps.so)
+LIB_PATH = os.environ.get("TMFWM_LIB") or os.path.join(_HERE, "libtmfwm.so")
 ABI_VERSION = 1
 
 MEM_HOST = 0
@@ -51,6 +53,21 @@ class TmfwmError(RuntimeError):
     """A HIP-side failure reported by libtmfwm.so."""
 
 
+def _share_hip_runtime() -> None:
+    """One HIP runtime per process.  PyTorch-ROCm bundles its own libamdhip64.so.7;
+    libtmfwm.so needs the same soname.  Whichever copy is loaded first is the one
+    every later user binds to, and torch does not work on a runtime other than its
+    own, so when torch is installed its copy is loaded (RTLD_GLOBAL) before this
+    library -- torch and libtmfwm then share one runtime in either import order.
+    Without torch the system ROCm runtime (/opt/rocm/lib) is used."""
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.submodule_search_locations:
+        return
+    path = os.path.join(list(spec.submodule_search_locations)[0], "lib", "libamdhip64.so")
+    if os.path.exists(path):
+        ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+
+
 def load():
     """Load and type the library once; raises ImportError if it was not built."""
     global _lib
@@ -63,6 +80,7 @@ def load():
                     f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
                     "or `make -C thatsmyface_amd/csrc` (hipcc, gfx950)"
                 )
+            _share_hip_runtime()
             L = ctypes.CDLL(LIB_PATH)
             for name, (res, args) in SIGNATURES.items():
                 fn = getattr(L, name)

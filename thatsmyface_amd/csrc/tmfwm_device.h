@@ -385,15 +385,27 @@ TMF_DEVI void dct3(float (&c)[N])
 }  // namespace dct
 
 // ---------------------------------------------------------------------------
-// Jacobi SVD (N5/N6) with B/L rows of A and V per lane, L lanes per block.
-// The op sequence is the oracle's: dot products are fma chains
-// over each lane's R contiguous rows, combined across the L lanes by an xor
-// butterfly (== balanced pairwise tree); round-robin pair schedule; rotation
-// iff g^2 > TOL2*a*b and g^2 > C*(a+b).
+// SVD (N5/N6), DESIGN.md 3.4: phase 1 f32 one-sided Jacobi (<= 4 sweeps) on D,
+// phase 2 two Bjorck steps on f64(V32), phase 3 f64 one-sided Jacobi on
+// A0 = D V0 to convergence.  B/L rows of A and V per lane, L lanes per block.
+// The op sequence is the oracle's: dot products are fma chains over each lane's
+// R contiguous rows, combined across the L lanes by an xor butterfly (== the
+// oracle's balanced pairwise tree); round-robin pair schedule; the rotation
+// tests and the IEEE-only rotation formula of oracle rotation()/rotationf().
 // ---------------------------------------------------------------------------
-constexpr int kMaxSweeps = 32;
-constexpr double kTol2 = 7.888609052210118e-31;  // 2^-100
-constexpr double kC2 = 9.860761315262648e-32;    // 2^-103
+template <typename T> struct JacP;
+template <> struct JacP<double> {
+    static constexpr int kMaxSweeps = 32;
+    static constexpr double kTol2 = 7.888609052210118e-31;  // 2^-100
+    static constexpr double kC2 = 9.860761315262648e-32;    // 2^-103
+};
+template <> struct JacP<float> {
+    static constexpr int kMaxSweeps = 4;
+    static constexpr float kTol2 = 9.094947017729282e-13f;  // 2^-40
+    static constexpr float kC2 = 2.842170943040401e-14f;    // 2^-45
+    static constexpr float kC2A = 3.552713678800501e-15f;   // 2^-48
+    static constexpr float kFMin = 9.313225746154785e-10f;  // 2^-30
+};
 
 // circle-method schedule: L = [0, 1 + (k-1+s) mod (b-1)], pair p = (L[p], L[b-1-p]) sorted
 template <int B>
@@ -416,173 +428,206 @@ TMF_DEVI void static_for(F &&f)
 }
 
 // ---- cross-lane moves inside a block group (DPP / ds_swizzle, no LDS traffic)
-template <int CTRL>
-TMF_DEVI double dpp_d(double v)
-{
-    const long long b = __builtin_bit_cast(long long, v);
-    const int lo = __builtin_amdgcn_mov_dpp((int)b, CTRL, 0xF, 0xF, false);
-    const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xF, 0xF, false);
-    return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
-}
-template <int PATTERN>
-TMF_DEVI double swz_d(double v)
-{
-    const long long b = __builtin_bit_cast(long long, v);
-    const int lo = __builtin_amdgcn_ds_swizzle((int)b, PATTERN);
-    const int hi = __builtin_amdgcn_ds_swizzle((int)(b >> 32), PATTERN);
-    return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
-}
+// DPP controls: quad_perm [1,0,3,2] = 0xB1 (xor 1), [2,3,0,1] = 0x4E (xor 2),
+// row_half_mirror = 0x141 (lane i <-> 7-i within 8 lanes).
 template <int CTRL>
 TMF_DEVI int dpp_i(int v) { return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, false); }
 template <int PATTERN>
 TMF_DEVI int swz_i(int v) { return __builtin_amdgcn_ds_swizzle(v, PATTERN); }
 
-// DPP controls: quad_perm [1,0,3,2] = 0xB1 (xor 1), [2,3,0,1] = 0x4E (xor 2),
-// row_half_mirror = 0x141 (lane i <-> 7-i within 8 lanes).
+template <int CTRL>
+TMF_DEVI double dpp(double v)
+{
+    const long long b = __builtin_bit_cast(long long, v);
+    const int lo = dpp_i<CTRL>((int)b), hi = dpp_i<CTRL>((int)(b >> 32));
+    return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+}
+template <int CTRL>
+TMF_DEVI float dpp(float v) { return __builtin_bit_cast(float, dpp_i<CTRL>(__builtin_bit_cast(int, v))); }
+
+template <int PATTERN>
+TMF_DEVI double swz(double v)
+{
+    const long long b = __builtin_bit_cast(long long, v);
+    const int lo = swz_i<PATTERN>((int)b), hi = swz_i<PATTERN>((int)(b >> 32));
+    return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+}
+template <int PATTERN>
+TMF_DEVI float swz(float v) { return __builtin_bit_cast(float, swz_i<PATTERN>(__builtin_bit_cast(int, v))); }
+
 // Butterfly sum over the L lanes of a group == the oracle's pairwise tree:
 // level 3 pairs lane i with 7-i, whose value (p6+p7)+(p4+p5) equals (p4+p5)+(p6+p7) bitwise.
-template <int L>
-TMF_DEVI double group_sum(double v)
+template <int L, typename T>
+TMF_DEVI T group_sum(T v)
 {
     static_assert(L == 1 || L == 2 || L == 4 || L == 8, "group size");
-    if constexpr (L >= 2) v = v + dpp_d<0xB1>(v);
-    if constexpr (L >= 4) v = v + dpp_d<0x4E>(v);
-    if constexpr (L >= 8) v = v + dpp_d<0x141>(v);
-    return v;
-}
-
-template <int CTRL>
-TMF_DEVI float dpp_f(float v)
-{
-    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
-}
-
-template <int L>
-TMF_DEVI float group_sum_f(float v)
-{
-    if constexpr (L >= 2) v = v + dpp_f<0xB1>(v);
-    if constexpr (L >= 4) v = v + dpp_f<0x4E>(v);
-    if constexpr (L >= 8) v = v + dpp_f<0x141>(v);
+    if constexpr (L >= 2) v = v + dpp<0xB1>(v);
+    if constexpr (L >= 4) v = v + dpp<0x4E>(v);
+    if constexpr (L >= 8) v = v + dpp<0x141>(v);
     return v;
 }
 
 // value of lane (group base + K) for every lane of the group
-template <int L, int K>
-TMF_DEVI double group_bcast(double v)
+template <int L, int K, typename T>
+TMF_DEVI T group_bcast(T v)
 {
     if constexpr (L == 1) return v;
-    else if constexpr (L == 2) return dpp_d<K == 0 ? 0xA0 : 0xF5>(v);                    // quad_perm [K,K,K+2,K+2]
-    else if constexpr (L == 4) return dpp_d<K | (K << 2) | (K << 4) | (K << 6)>(v);      // quad_perm [K,K,K,K]
-    else return swz_d<(K << 5) | 0x18>(v);                                                // bitmask: (lane & 0x18) | K
-}
-template <int L, int K>
-TMF_DEVI int group_bcast_i(int v)
-{
-    if constexpr (L == 1) return v;
-    else if constexpr (L == 2) return dpp_i<K == 0 ? 0xA0 : 0xF5>(v);
-    else if constexpr (L == 4) return dpp_i<K | (K << 2) | (K << 4) | (K << 6)>(v);
-    else return swz_i<(K << 5) | 0x18>(v);
+    else if constexpr (L == 2) return dpp<K == 0 ? 0xA0 : 0xF5>(v);                    // quad_perm [K,K,K+2,K+2]
+    else if constexpr (L == 4) return dpp<K | (K << 2) | (K << 4) | (K << 6)>(v);      // quad_perm [K,K,K,K]
+    else return swz<(K << 5) | 0x18>(v);                                                // bitmask: (lane & 0x18) | K
 }
 
-// sum over rows of A[:,i]*A[:,j] in the contract order
-template <int R, int B, int L>
-TMF_DEVI double cdot(const double (&A)[R][B], int i, int j)
+TMF_DEVI double fma_t(double a, double b, double c) { return __builtin_fma(a, b, c); }
+TMF_DEVI float fma_t(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+TMF_DEVI double abs_t(double a) { return __builtin_fabs(a); }
+TMF_DEVI float abs_t(float a) { return __builtin_fabsf(a); }
+TMF_DEVI double sign1_t(double d) { return __builtin_copysign(1.0, d); }
+TMF_DEVI float sign1_t(float d) { return __builtin_copysignf(1.0f, d); }
+
+// sum over rows of A[:,i]*A[:,j] in the contract order (oracle cdot / cdotf)
+template <int R, int B, int L, typename T>
+TMF_DEVI T cdot(const T (&A)[R][B], int i, int j)
 {
-    double acc = 0.0;
+    T acc = T(0);
 #pragma unroll
-    for (int r = 0; r < R; ++r) acc = __builtin_fma(A[r][i], A[r][j], acc);
+    for (int r = 0; r < R; ++r) acc = fma_t(A[r][i], A[r][j], acc);
     return group_sum<L>(acc);
 }
-
-struct Rot {
-    double c, s, tg;
-};
 
 // Bitwise blend with an opaque lane mask: keeps the selection a v_bfi_b32 on values,
 // so the optimiser cannot turn "pick nrm[i] by lane" into a dynamically indexed
 // (scratch) array access.
-TMF_DEVI double blend_d(int mask, double x, double y)
+TMF_DEVI double blend(int mask, double x, double y)
 {
     const long long m = (long long)mask;  // 0 or -1
     const long long xb = __builtin_bit_cast(long long, x), yb = __builtin_bit_cast(long long, y);
     return __builtin_bit_cast(double, (xb & m) | (yb & ~m));
 }
-
-// Rotation of a pair (oracle rotation()): 2 sqrt + 1 divide.
-TMF_DEVI Rot rotation(double alpha, double beta, double gamma)
+TMF_DEVI float blend(int mask, float x, float y)
 {
-    Rot o;
-    const double d = beta - alpha;
-    const double g = gamma + gamma;
-    const double r = __builtin_sqrt(__builtin_fma(d, d, g * g));
-    const double w = __builtin_fabs(d) + r;
-    const double q = 1.0 / __builtin_sqrt((r + r) * w);
-    const double sg = __builtin_copysign(1.0, d);
+    const int xb = __builtin_bit_cast(int, x), yb = __builtin_bit_cast(int, y);
+    return __builtin_bit_cast(float, (xb & mask) | (yb & ~mask));
+}
+
+// 1/sqrt(x) from IEEE ops only (oracle rsqrt_n / rsqrtf_n): integer seed + Newton
+TMF_DEVI double rsqrt_n(double x)
+{
+    const unsigned long long i = 0x5fe6eb50c7b537a9ull - (__builtin_bit_cast(unsigned long long, x) >> 1);
+    double y = __builtin_bit_cast(double, i);
+    const double hx = 0.5 * x;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const double t = y * y;
+        const double u = __builtin_fma(-hx, t, 1.5);
+        y = y * u;
+    }
+    return y;
+}
+TMF_DEVI float rsqrt_n(float x)
+{
+    const unsigned i = 0x5f375a86u - (__builtin_bit_cast(unsigned, x) >> 1);
+    float y = __builtin_bit_cast(float, i);
+    const float hx = 0.5f * x;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float t = y * y;
+        const float u = __builtin_fmaf(-hx, t, 1.5f);
+        y = y * u;
+    }
+    return y;
+}
+
+template <typename T>
+struct Rot {
+    T c, s, tg;
+};
+
+// Rotation of a pair (oracle rotation() / rotationf())
+template <typename T>
+TMF_DEVI Rot<T> rotation(T alpha, T beta, T gamma)
+{
+    Rot<T> o;
+    const T d = beta - alpha;
+    const T g = gamma + gamma;
+    const T x = fma_t(d, d, g * g);
+    const T r = x * rsqrt_n(x);
+    const T w = abs_t(d) + r;
+    const T q = rsqrt_n((r + r) * w);
+    const T sg = sign1_t(d);
     o.c = w * q;
     o.s = (g * sg) * q;
     o.tg = (((g * g) * r) * (q * q)) * sg;
     return o;
 }
 
-TMF_DEVI bool rotate_test(double alpha, double beta, double gamma, double c2)
+// One-sided Jacobi on A (and V when WANT_V) in precision T.  Returns this block's
+// sweep count exactly as the oracle counts it (sweeps up to and including the
+// first one without a rotation, capped at the precision's maximum); the wave runs
+// until its slowest block stops -- further sweeps of a converged block are
+// no-ops (same A, same tests, no rotation).  Pairs of a round are disjoint, so
+// they are applied in any order.  Every lane of a group holds the column norms;
+// lane q evaluates the rotations of pairs [q*PP, q*PP+PP) and broadcasts
+// (c, s, t*gamma).  Updates run under an exec mask (never if-converted): lanes
+// of blocks that skip a pair keep their bits.
+template <typename T, int B, int L, bool WANT_V>
+TMF_DEVI int jacobi(T (&A)[B / L][B], T (&V)[B / L][B], int q)
 {
-    const double g2 = gamma * gamma;
-    return !(g2 <= c2 * (alpha + beta) || g2 <= (kTol2 * alpha) * beta);
-}
-
-// One-sided Jacobi on A (and V when WANT_V).  Returns sweeps executed by the wave.
-// Pairs of a round are disjoint, so they are applied in any order.  Every lane of
-// a group holds the column norms; lane q evaluates the rotations of pairs
-// [q*PP, q*PP+PP) and broadcasts (c, s, t*gamma).  Updates run under an exec
-// mask (never if-converted): lanes of blocks that skip a pair keep their bits.
-template <int B, int L, bool WANT_V>
-TMF_DEVI int jacobi(double (&A)[B / L][B], double (&V)[B / L][B], int q)
-{
+    using P = JacP<T>;
     constexpr int R = B / L, NP = B / 2, PP = NP / L;
     static_assert(PP >= 1, "need L <= B/2");
-    double F = 0.0;
+    T F = T(0);
     static_for<B>([&](auto K) { F += cdot<R, B, L>(A, K, K); });
-    const double c2 = kC2 * F;
-    int sweep = 0;
-    for (; sweep < kMaxSweeps; ++sweep) {
-        double nrm[B];
+    const T c2 = P::kC2 * F;
+    T c2a = T(0);
+    bool live = true;
+    if constexpr (std::is_same_v<T, float>) {
+        c2a = P::kC2A * (F * F);
+        live = F >= P::kFMin;  // oracle jacobi_f32: return 0 (no sweep) below 2^-30
+    }
+    int count = 0;
+    bool active = live;
+    for (int sweep = 0; sweep < P::kMaxSweeps; ++sweep) {
+        T nrm[B];
         static_for<B>([&](auto K) { nrm[K] = cdot<R, B, L>(A, K, K); });
         int rotated = 0;
         static_for<B - 1>([&](auto S) {
             constexpr int s = S;
-            double ga[NP];
+            T ga[NP];
             bool on[NP];
-            static_for<NP>([&](auto P) {
-                constexpr int p = P, i = Sched<B>::lo(s, p), j = Sched<B>::hi(s, p);
+            static_for<NP>([&](auto Pi) {
+                constexpr int p = Pi, i = Sched<B>::lo(s, p), j = Sched<B>::hi(s, p);
                 ga[p] = cdot<R, B, L>(A, i, j);
-                on[p] = rotate_test(nrm[i], nrm[j], ga[p], c2);
+                const T g2 = ga[p] * ga[p];
+                bool skip = g2 <= c2 * (nrm[i] + nrm[j]) || g2 <= (P::kTol2 * nrm[i]) * nrm[j];
+                if constexpr (std::is_same_v<T, float>) skip = skip || g2 <= c2a || !live;
+                on[p] = !skip;
             });
             // parameters of this lane's pairs
-            Rot mine[PP];
+            Rot<T> mine[PP];
             static_for<PP>([&](auto U) {
                 constexpr int p0 = U, i0 = Sched<B>::lo(s, p0), j0 = Sched<B>::hi(s, p0);
-                double a = nrm[i0], b = nrm[j0], g = ga[p0];
+                T a = nrm[i0], b = nrm[j0], g = ga[p0];
                 bool o = on[p0];
                 static_for<L - 1>([&](auto Q1) {
                     constexpr int QQ = Q1 + 1, p = QQ * PP + U, i = Sched<B>::lo(s, p), j = Sched<B>::hi(s, p);
                     int m = -(int)(q == QQ);
                     asm volatile("" : "+v"(m));
-                    a = blend_d(m, nrm[i], a);
-                    b = blend_d(m, nrm[j], b);
-                    g = blend_d(m, ga[p], g);
+                    a = blend(m, nrm[i], a);
+                    b = blend(m, nrm[j], b);
+                    g = blend(m, ga[p], g);
                     o = (m & (int)on[p]) | (~m & (int)o);
                 });
-                mine[U] = Rot{1.0, 0.0, 0.0};
+                mine[U] = Rot<T>{T(1), T(0), T(0)};
                 if (o) {
                     asm volatile("" ::: "memory");
                     mine[U] = rotation(a, b, g);
                 }
             });
-            static_for<NP>([&](auto P) {
-                constexpr int p = P, i = Sched<B>::lo(s, p), j = Sched<B>::hi(s, p), u = p % PP, src = p / PP;
-                const double c = group_bcast<L, src>(mine[u].c);
-                const double sn = group_bcast<L, src>(mine[u].s);
-                const double tg = group_bcast<L, src>(mine[u].tg);
+            static_for<NP>([&](auto Pi) {
+                constexpr int p = Pi, i = Sched<B>::lo(s, p), j = Sched<B>::hi(s, p), u = p % PP, src = p / PP;
+                const T c = group_bcast<L, src>(mine[u].c);
+                const T sn = group_bcast<L, src>(mine[u].s);
+                const T tg = group_bcast<L, src>(mine[u].tg);
                 if (on[p]) {
                     asm volatile("" ::: "memory");
                     rotated = 1;
@@ -590,27 +635,113 @@ TMF_DEVI int jacobi(double (&A)[B / L][B], double (&V)[B / L][B], int q)
                     nrm[j] = nrm[j] + tg;
 #pragma unroll
                     for (int r = 0; r < R; ++r) {
-                        const double x = A[r][i], y = A[r][j];
-                        A[r][i] = __builtin_fma(-sn, y, c * x);
-                        A[r][j] = __builtin_fma(sn, x, c * y);
+                        const T x = A[r][i], y = A[r][j];
+                        A[r][i] = fma_t(-sn, y, c * x);
+                        A[r][j] = fma_t(sn, x, c * y);
                     }
                     if constexpr (WANT_V) {
 #pragma unroll
                         for (int r = 0; r < R; ++r) {
-                            const double x = V[r][i], y = V[r][j];
-                            V[r][i] = __builtin_fma(-sn, y, c * x);
-                            V[r][j] = __builtin_fma(sn, x, c * y);
+                            const T x = V[r][i], y = V[r][j];
+                            V[r][i] = fma_t(-sn, y, c * x);
+                            V[r][j] = fma_t(sn, x, c * y);
                         }
                     }
                 }
             });
         });
-        if (!__any(rotated)) {
-            ++sweep;
-            break;
-        }
+        count += active ? 1 : 0;
+        active = active && rotated;
+        if (!__any(rotated)) break;
     }
-    return sweep;
+    return count;
+}
+
+// Phase 2 (oracle bjorck()): V <- V N, N = 1.5 I - 0.5 V^T V, computed column by
+// column of N (N is symmetric; cdot(V, j, k) == cdot(V, k, j) bitwise).
+template <int B, int L>
+TMF_DEVI void bjorck(double (&V)[B / L][B])
+{
+    constexpr int R = B / L;
+    double T[R][B];
+    static_for<B>([&](auto K) {
+        constexpr int k = K;
+        double n[B];
+        static_for<B>([&](auto J) {
+            constexpr int j = J;
+            const double qv = cdot<R, B, L>(V, j, k);
+            n[j] = (j == k) ? __builtin_fma(-0.5, qv, 1.5) : -0.5 * qv;
+        });
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            double acc = 0.0;
+#pragma unroll
+            for (int j = 0; j < B; ++j) acc = __builtin_fma(V[r][j], n[j], acc);
+            T[r][k] = acc;
+        }
+    });
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int k = 0; k < B; ++k) V[r][k] = T[r][k];
+}
+
+// A0 = D V (oracle: fma chain over j = 0..b-1); row j of V comes from lane j / R.
+template <int B, int L>
+TMF_DEVI void mul_dv(const float (&D)[B / L][B], const double (&V)[B / L][B], double (&A)[B / L][B])
+{
+    constexpr int R = B / L;
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int k = 0; k < B; ++k) A[r][k] = 0.0;
+    static_for<B>([&](auto J) {
+        constexpr int j = J, src = j / R, jr = j % R;
+        double vrow[B];
+#pragma unroll
+        for (int k = 0; k < B; ++k) vrow[k] = group_bcast<L, src>(V[jr][k]);
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int k = 0; k < B; ++k) A[r][k] = __builtin_fma((double)D[r][j], vrow[k], A[r][k]);
+    });
+}
+
+// Full SVD of this lane's rows of D (oracle orc_svd_block, phases 1-3): on return A
+// holds A V (columns = sigma_k u_k), V the right singular vectors (unsorted).
+// Returns f64 sweeps | (f32 sweeps << 8) of this block.
+struct NoStamp {
+    TMF_DEVI void operator()(int) const {}
+};
+
+template <int B, int L, typename Stamp = NoStamp>
+TMF_DEVI int svd3(const float (&D)[B / L][B], double (&A)[B / L][B], double (&V)[B / L][B], int q, Stamp stamp = {})
+{
+    constexpr int R = B / L;
+    int s32;
+    {
+        float A32[R][B], V32[R][B];
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int c = 0; c < B; ++c) {
+                A32[r][c] = D[r][c];
+                V32[r][c] = (q * R + r == c) ? 1.0f : 0.0f;
+            }
+        s32 = jacobi<float, B, L, true>(A32, V32, q);
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int c = 0; c < B; ++c) V[r][c] = (double)V32[r][c];
+    }
+    stamp(1);
+    bjorck<B, L>(V);
+    bjorck<B, L>(V);
+    mul_dv<B, L>(D, V, A);
+    stamp(2);
+    const int s64 = jacobi<double, B, L, true>(A, V, q);
+    stamp(3);
+    return s64 | (s32 << 8);
 }
 
 // ---------------------------------------------------------------------------
@@ -648,7 +779,7 @@ TMF_DEVI bool sigma1_certified(const float (&x)[B / L][B], float &s1)
             float acc = 0.0f;
 #pragma unroll
             for (int r = 0; r < R; ++r) acc = __builtin_fmaf(x[r][j], uu[r], acc);
-            w[j] = group_sum_f<L>(acc);
+            w[j] = group_sum<L>(acc);
             nn = __builtin_fmaf(w[j], w[j], nn);
         }
         const bool live = nn > 1e-30f;

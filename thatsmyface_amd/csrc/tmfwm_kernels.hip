@@ -18,6 +18,24 @@
 
 namespace tmf {
 
+// Opt-in phase profile (make stamps): per-wave s_memtime deltas summed per phase.
+#ifdef TMF_STAMPS
+__device__ unsigned long long g_stamps[16];
+struct Stamp {
+    unsigned long long *t;
+    TMF_DEVI void operator()(int k) const
+    {
+        const unsigned long long now = __builtin_amdgcn_s_memtime();
+        if ((threadIdx.x & 63) == 0 && (blockIdx.x & 63) == 0) atomicAdd(&g_stamps[k], now - *t);  // 1/64 of the waves
+        *t = now;
+    }
+};
+#define TMF_STAMP_INIT unsigned long long tmf_t0 = __builtin_amdgcn_s_memtime(); const Stamp stamp{&tmf_t0}
+#else
+using Stamp = NoStamp;
+#define TMF_STAMP_INIT const Stamp stamp{}
+#endif
+
 template <int B>
 struct Geo {
     static constexpr int L = (B == 16) ? 8 : (B == 8) ? 2 : 1;  // lanes per block (== oracle jac_chunks)
@@ -160,6 +178,7 @@ __global__ __launch_bounds__(64) void embed_kernel(EmbedArgs a)
     const uint8_t *src = a.src + pos.frame * a.frame_stride;
     uint8_t *dst = a.dst + pos.frame * a.frame_stride;
 
+    TMF_STAMP_INIT;
     float x[R][B];
     {
         uint32_t words[R][NW];
@@ -171,16 +190,10 @@ __global__ __launch_bounds__(64) void embed_kernel(EmbedArgs a)
             for (int i = 0; i < NW; ++i) pix[r * NW + i][lane] = words[r][i];
     }
     dct2d_rows_layout<B, false>(x, tile, q);  // :192
+    stamp(0);
 
     double A[R][B], V[R][B];
-#pragma unroll
-    for (int r = 0; r < R; ++r)
-#pragma unroll
-        for (int c = 0; c < B; ++c) {
-            A[r][c] = (double)x[r][c];
-            V[r][c] = (q * R + r == c) ? 1.0 : 0.0;
-        }
-    jacobi<B, L, true>(A, V, q);  // :195 (SVD)
+    svd3<B, L>(x, A, V, q, stamp);  // :195 (SVD)
 
     // singular values, U = A / sigma, sort descending (oracle orc_svd_block)
     double sig[B];
@@ -248,7 +261,9 @@ __global__ __launch_bounds__(64) void embed_kernel(EmbedArgs a)
         for (int j = 0; j < B; ++j) x[r][j] = m[j];
     }
     __syncthreads();
+    stamp(4);
     dct2d_rows_layout<B, true>(x, tile, q);  // :204
+    stamp(5);
 
     // :207-216 write back and ycbcr_to_rgb with this lane's original chroma
     if (pos.valid) {
@@ -277,6 +292,7 @@ __global__ __launch_bounds__(64) void embed_kernel(EmbedArgs a)
             store_words<Geo<B>::NW>(p, a.aligned, out);
         }
     }
+    stamp(6);
 }
 
 // ---------------------------------------------------------------------------
@@ -303,7 +319,7 @@ TMF_DEVI float sigma1_of(const uint8_t *frame_base, int W, const StripPos &pos, 
         for (int r = 0; r < R; ++r)
 #pragma unroll
             for (int c = 0; c < B; ++c) A[r][c] = ok ? 0.0 : (double)x[r][c];
-        jacobi<B, L, false>(A, V, q);
+        jacobi<double, B, L, false>(A, V, q);
         double m = 0.0;
 #pragma unroll
         for (int k = 0; k < B; ++k) {
@@ -418,15 +434,13 @@ __global__ __launch_bounds__(64) void svd_blocks_kernel(const float *__restrict_
     const int lane = threadIdx.x & 63, g = lane / L, q = lane % L;
     const int64_t blk = (int64_t)blockIdx.x * BPW + g;
     const bool valid = blk < nblocks;
-    double A[R][B], V[R][B];
+    float x[R][B];
 #pragma unroll
     for (int r = 0; r < R; ++r)
 #pragma unroll
-        for (int c = 0; c < B; ++c) {
-            A[r][c] = valid ? (double)D[blk * B * B + (q * R + r) * B + c] : 0.0;
-            V[r][c] = (q * R + r == c) ? 1.0 : 0.0;
-        }
-    const int nsw = jacobi<B, L, true>(A, V, q);
+        for (int c = 0; c < B; ++c) x[r][c] = valid ? D[blk * B * B + (q * R + r) * B + c] : 0.0f;
+    double A[R][B], V[R][B];
+    int nsw = svd3<B, L>(x, A, V, q);
     double sig[B];
     float Uf[R][B], Vf[R][B];
 #pragma unroll
@@ -443,6 +457,7 @@ __global__ __launch_bounds__(64) void svd_blocks_kernel(const float *__restrict_
 #pragma unroll
     for (int k = 0; k < B; ++k) zero = zero && (sig[k] == 0.0);
     if (zero) {
+        nsw = 0;  // oracle: D == 0 returns before any sweep
 #pragma unroll
         for (int r = 0; r < R; ++r)
 #pragma unroll
@@ -644,6 +659,18 @@ hipError_t launch_svd_blocks(const float *D, int64_t nb, int block, float *U, fl
     default: return hipErrorInvalidValue;
     }
 }
+
+#ifdef TMF_STAMPS
+extern "C" int tmfwm_debug_stamps(unsigned long long *out, int reset)
+{
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 16) != hipSuccess) return -5;
+    if (reset) {
+        unsigned long long z[16] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof z) != hipSuccess) return -5;
+    }
+    return 0;
+}
+#endif
 
 hipError_t launch_synth(uint64_t seed, int64_t frame0, int64_t nframes, int64_t frame_bytes, uint8_t *out, hipStream_t st)
 {
