@@ -393,14 +393,30 @@ TMF_DEVI void dct3(float (&c)[N])
 // oracle's balanced pairwise tree); round-robin pair schedule; the rotation
 // tests and the IEEE-only rotation formula of oracle rotation()/rotationf().
 // ---------------------------------------------------------------------------
+// TMF_F32_SWEEPS / TMF_F64_SWEEPS override the sweep caps for timing experiments
+// only (tools/time_embed.py); the contract values are the defaults.
+#ifndef TMF_F32_SWEEPS
+#define TMF_F32_SWEEPS 4
+#endif
+#ifndef TMF_F64_SWEEPS
+#define TMF_F64_SWEEPS 32
+#endif
+#ifndef TMF_F64_BRANCHY
+#define TMF_F64_BRANCHY 1
+#endif
+// kBranchy: skip a pair's rotation / update when no block of the wave rotates it
+// (pays off in the converging f64 sweeps); branch-free otherwise (the f32 sweeps
+// rotate nearly every pair somewhere in the wave, and a join costs register moves).
 template <typename T> struct JacP;
 template <> struct JacP<double> {
-    static constexpr int kMaxSweeps = 32;
+    static constexpr bool kBranchy = TMF_F64_BRANCHY;
+    static constexpr int kMaxSweeps = TMF_F64_SWEEPS;
     static constexpr double kTol2 = 7.888609052210118e-31;  // 2^-100
     static constexpr double kC2 = 9.860761315262648e-32;    // 2^-103
 };
 template <> struct JacP<float> {
-    static constexpr int kMaxSweeps = 4;
+    static constexpr bool kBranchy = false;
+    static constexpr int kMaxSweeps = TMF_F32_SWEEPS;
     static constexpr float kTol2 = 9.094947017729282e-13f;  // 2^-40
     static constexpr float kC2 = 2.842170943040401e-14f;    // 2^-45
     static constexpr float kC2A = 3.552713678800501e-15f;   // 2^-48
@@ -567,8 +583,10 @@ TMF_DEVI Rot<T> rotation(T alpha, T beta, T gamma)
 // no-ops (same A, same tests, no rotation).  Pairs of a round are disjoint, so
 // they are applied in any order.  Every lane of a group holds the column norms;
 // lane q evaluates the rotations of pairs [q*PP, q*PP+PP) and broadcasts
-// (c, s, t*gamma).  Updates run under an exec mask (never if-converted): lanes
-// of blocks that skip a pair keep their bits.
+// (c, s, t*gamma).  Rotation and update branches are wave-uniform (__any): a pair
+// no block of the wave rotates costs nothing, and inside the branch lanes whose
+// block skips it apply the bitwise-exact identity (no divergent exec masks, so
+// the updates stay in place instead of being computed aside and copied back).
 template <typename T, int B, int L, bool WANT_V>
 TMF_DEVI int jacobi(T (&A)[B / L][B], T (&V)[B / L][B], int q)
 {
@@ -618,9 +636,11 @@ TMF_DEVI int jacobi(T (&A)[B / L][B], T (&V)[B / L][B], int q)
                     o = (m & (int)on[p]) | (~m & (int)o);
                 });
                 mine[U] = Rot<T>{T(1), T(0), T(0)};
-                if (o) {
-                    asm volatile("" ::: "memory");
-                    mine[U] = rotation(a, b, g);
+                if (!P::kBranchy || __any(o)) {  // wave-uniform: every lane computes, non-rotating lanes keep identity
+                    const Rot<T> r = rotation(a, b, g);
+                    mine[U].c = o ? r.c : T(1);
+                    mine[U].s = o ? r.s : T(0);
+                    mine[U].tg = o ? r.tg : T(0);
                 }
             });
             static_for<NP>([&](auto Pi) {
@@ -628,9 +648,12 @@ TMF_DEVI int jacobi(T (&A)[B / L][B], T (&V)[B / L][B], int q)
                 const T c = group_bcast<L, src>(mine[u].c);
                 const T sn = group_bcast<L, src>(mine[u].s);
                 const T tg = group_bcast<L, src>(mine[u].tg);
-                if (on[p]) {
-                    asm volatile("" ::: "memory");
-                    rotated = 1;
+                rotated |= (int)on[p];
+                // Wave-uniform branch; lanes whose block skips this pair apply the identity
+                // (c, s, t*gamma) = (1, 0, 0): fma(-0, y, 1*x) == x bitwise for every value
+                // A (phase 3) and V can hold (their fma chains start from +0 and never make
+                // -0), and A32 / phase-1 A only feed cdot(), which ignores signs of zero.
+                if (!P::kBranchy || __any(on[p])) {
                     nrm[i] = nrm[i] - tg;
                     nrm[j] = nrm[j] + tg;
 #pragma unroll
@@ -657,26 +680,55 @@ TMF_DEVI int jacobi(T (&A)[B / L][B], T (&V)[B / L][B], int q)
     return count;
 }
 
-// Phase 2 (oracle bjorck()): V <- V N, N = 1.5 I - 0.5 V^T V, computed column by
-// column of N (N is symmetric; cdot(V, j, k) == cdot(V, k, j) bitwise).
+// Phase 2 (oracle bjorck()): V <- V N, N = 1.5 I - 0.5 V^T V.  N is symmetric and
+// cdot(V, j, k) == cdot(V, k, j) bitwise, so only the upper triangle is computed.
 template <int B, int L>
 TMF_DEVI void bjorck(double (&V)[B / L][B])
 {
     constexpr int R = B / L;
+    if constexpr (B > 8) {  // 136 packed doubles would not fit in registers: column by column
+        double T[R][B];
+        static_for<B>([&](auto K) {
+            constexpr int k = K;
+            double n[B];
+            static_for<B>([&](auto J) {
+                constexpr int j = J;
+                const double qv = cdot<R, B, L>(V, j, k);
+                n[j] = (j == k) ? __builtin_fma(-0.5, qv, 1.5) : -0.5 * qv;
+            });
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                double acc = 0.0;
+#pragma unroll
+                for (int j = 0; j < B; ++j) acc = __builtin_fma(V[r][j], n[j], acc);
+                T[r][k] = acc;
+            }
+        });
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int k = 0; k < B; ++k) V[r][k] = T[r][k];
+        return;
+    }
+    double N[B * (B + 1) / 2];  // packed upper triangle, row j: N[j][k], k >= j
+    static_for<B>([&](auto J) {
+        constexpr int j = J;
+        static_for<B - j>([&](auto K0) {
+            constexpr int k = j + K0, idx = j * B - j * (j - 1) / 2 + K0;
+            const double qv = cdot<R, B, L>(V, j, k);
+            N[idx] = (j == k) ? __builtin_fma(-0.5, qv, 1.5) : -0.5 * qv;
+        });
+    });
     double T[R][B];
     static_for<B>([&](auto K) {
         constexpr int k = K;
-        double n[B];
-        static_for<B>([&](auto J) {
-            constexpr int j = J;
-            const double qv = cdot<R, B, L>(V, j, k);
-            n[j] = (j == k) ? __builtin_fma(-0.5, qv, 1.5) : -0.5 * qv;
-        });
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             double acc = 0.0;
-#pragma unroll
-            for (int j = 0; j < B; ++j) acc = __builtin_fma(V[r][j], n[j], acc);
+            static_for<B>([&](auto J) {
+                constexpr int j = J, lo = j < k ? j : k, hi = j < k ? k : j;
+                acc = __builtin_fma(V[r][j], N[lo * B - lo * (lo - 1) / 2 + (hi - lo)], acc);
+            });
             T[r][k] = acc;
         }
     });
