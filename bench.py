@@ -41,7 +41,8 @@ def parse():
     p.add_argument("--width", type=int, default=3840)
     p.add_argument("--block", type=int, default=8)
     p.add_argument("--alpha", type=float, default=0.1)
-    p.add_argument("--cpu-frames", type=int, default=2, help="frames in the CPU-baseline sample (0 = skip)")
+    p.add_argument("--cpu-frames", type=int, default=48,
+                   help="frames in the CPU-baseline sample, ~10 s of oracle work on 16 cores (0 = skip)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     return p.parse_args()
 
@@ -133,7 +134,7 @@ def main():
     achieved = embed_bytes / (embed_ms * 1e-3) / 1e9
 
     traffic = None
-    tp = os.path.join(ROOT, "profiles", "traffic_r01.json")
+    tp = os.path.join(ROOT, "profiles", "traffic.json")
     if os.path.exists(tp):
         try:
             with open(tp) as f:
@@ -145,7 +146,7 @@ def main():
             traffic = None
 
     cpu = None
-    if rank == 0 and not args.no_cpu_baseline and args.cpu_frames > 0:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_frames > 0:
         k = min(args.cpu_frames, F)
         cpu = cpu_baseline(frames[:k].cpu().numpy(), wm.cpu().numpy(), b, alpha)
 

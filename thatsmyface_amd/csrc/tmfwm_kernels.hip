@@ -298,14 +298,15 @@ __global__ __launch_bounds__(64) void embed_kernel(EmbedArgs a)
 // ---------------------------------------------------------------------------
 // Extract: watermarking.py:241-289 fused; sigma_1 of both images per block.
 // ---------------------------------------------------------------------------
-constexpr int kPowerIters = 6;  // f32 power iterations before certification
+#ifndef TMF_POWER_ITERS
+#define TMF_POWER_ITERS 6
+#endif
+constexpr int kPowerIters = TMF_POWER_ITERS;  // f32 power iterations before certification
 
 template <int B>
-TMF_DEVI float sigma1_of(const uint8_t *frame_base, int W, const StripPos &pos, int q, bool aligned, float *tile)
+TMF_DEVI float sigma1_of(const uint32_t (&words)[Geo<B>::R][Geo<B>::NW], int q, float *tile)
 {
     constexpr int L = Geo<B>::L, R = Geo<B>::R;
-    uint32_t words[R][Geo<B>::NW];
-    load_block_rows<B>(frame_base, W, pos, q, aligned, words);
     float x[R][B];
     luma_rows<B>(words, x);
     dct2d_rows_layout<B, false>(x, tile, q);
@@ -339,8 +340,12 @@ __global__ __launch_bounds__(64) void extract_kernel(ExtractArgs a)
     const int lane = threadIdx.x & 63, g = lane / L, q = lane % L;
     float *tile = lds + g * B * LD;
     const StripPos pos = strip_pos<B>(a.strips_per_row, a.nbw);
-    const float sw = sigma1_of<B>(a.wsrc + pos.frame * a.frame_stride, a.W, pos, q, a.aligned, tile);
-    const float so = sigma1_of<B>(a.osrc + pos.frame * a.frame_stride, a.W, pos, q, a.aligned, tile);
+    // both images' rows are requested up front: one exposed HBM latency per wave, not two
+    uint32_t ww[Geo<B>::R][Geo<B>::NW], wo[Geo<B>::R][Geo<B>::NW];
+    load_block_rows<B>(a.wsrc + pos.frame * a.frame_stride, a.W, pos, q, a.aligned, ww);
+    load_block_rows<B>(a.osrc + pos.frame * a.frame_stride, a.W, pos, q, a.aligned, wo);
+    const float sw = sigma1_of<B>(ww, q, tile);
+    const float so = sigma1_of<B>(wo, q, tile);
     // :285 under numpy-2 NEP 50: (f32 - f32) / f32(alpha) in f32; :288-289 clip, *255 in f64, trunc
     const float e = (sw - so) / a.alpha32;
     double d = (double)e;
