@@ -76,21 +76,31 @@ static inline void colour_inv(float y, float cbs, float crs, uint8_t out[3])
 }
 
 /* ------------------------------------------------------------------------ */
-/* N3: pocketfft fp32 DCT-II / DCT-III (ortho), lengths 4, 8, 16             */
+/* N3: pocketfft fp32 DCT-II / DCT-III (ortho), every even length 4..16     */
+/* (the UI block sizes, embed_watermark_page.py:324-331).                    */
 /* scipy.fftpack.dct/idct -> pocketfft T_dcst23::exec around rfftp.          */
 /* Every statement below is one fp32 operation (no contraction).             */
 /* ------------------------------------------------------------------------ */
 typedef struct {
     int n;
     int nf;
-    int fct[4];            /* rfftp factor list, factor 2 first (pocketfft factorize) */
+    int fct[4];            /* rfftp factor list (pocketfft factorize: 4s, then a 2 moved to the front, then odd) */
     float tw[4][3 * 16];   /* rfftp twiddles per factor: tw[k][(j-1)*(ido-1) + 2i-2 / 2i-1] */
+    float tws[4][2 * 16];  /* generic-radix (ip > 5) table: tws[2m], tws[2m+1] = cos, sin(2 pi m / ip) */
     float dtw[16];         /* DCT twiddle[i] = cos(2 pi (i+1) / (4n)) */
     float norm;            /* f32(1/sqrt(2n)) (scipy norm_fct, ortho) */
 } dct_plan;
 
-static dct_plan g_plans[3];
+#define ORC_NPLANS 7 /* n = 4, 6, ..., 16 */
+static dct_plan g_plans[ORC_NPLANS];
 static int g_plans_ready = 0;
+
+static const long double ORC_PI = 3.141592653589793238462643383279502884L;
+
+/* comp_twiddle's twid[m] = (cos 2 pi m / n, sin 2 pi m / n): pocketfft's sincos_2pibyn
+ * computes them in double for a float plan and rounds; long double here, same floats */
+static float tw_cos(long m, long n) { return (float)(double)cosl(2.0L * ORC_PI * (long double)m / (long double)n); }
+static float tw_sin(long m, long n) { return (float)(double)sinl(2.0L * ORC_PI * (long double)m / (long double)n); }
 
 static void plan_init(dct_plan *p, int n)
 {
@@ -103,41 +113,47 @@ static void plan_init(dct_plan *p, int n)
         p->fct[nf++] = 2;
         int t = p->fct[0]; p->fct[0] = p->fct[nf - 1]; p->fct[nf - 1] = t;
     }
+    for (int d = 3; d * d <= len; d += 2)
+        while (len % d == 0) { p->fct[nf++] = d; len /= d; }
+    if (len > 1) p->fct[nf++] = len;
     p->nf = nf;
-    /* comp_twiddle: twid[m] = (cos 2 pi m / n, sin 2 pi m / n), computed in high precision */
     int l1 = 1;
     for (int k = 0; k < nf; ++k) {
         int ip = p->fct[k], ido = n / (l1 * ip);
         if (k < nf - 1) {
             for (int j = 1; j < ip; ++j)
                 for (int i = 1; i <= (ido - 1) / 2; ++i) {
-                    long double ang = 2.0L * 3.141592653589793238462643383279502884L * (long double)(j * l1 * i) / (long double)n;
-                    p->tw[k][(j - 1) * (ido - 1) + 2 * i - 2] = (float)(double)cosl(ang);
-                    p->tw[k][(j - 1) * (ido - 1) + 2 * i - 1] = (float)(double)sinl(ang);
+                    p->tw[k][(j - 1) * (ido - 1) + 2 * i - 2] = tw_cos(j * l1 * i, n);
+                    p->tw[k][(j - 1) * (ido - 1) + 2 * i - 1] = tw_sin(j * l1 * i, n);
                 }
+        }
+        if (ip > 5) {
+            p->tws[k][0] = 1.0f;
+            p->tws[k][1] = 0.0f;
+            for (int i = 2, ic = 2 * ip - 2; i <= ic; i += 2, ic -= 2) {
+                p->tws[k][i] = tw_cos(i / 2 * (n / ip), n);
+                p->tws[k][i + 1] = tw_sin(i / 2 * (n / ip), n);
+                p->tws[k][ic] = tw_cos(i / 2 * (n / ip), n);
+                p->tws[k][ic + 1] = -tw_sin(i / 2 * (n / ip), n);
+            }
         }
         l1 *= ip;
     }
-    for (int i = 0; i < n; ++i) {
-        long double ang = 2.0L * 3.141592653589793238462643383279502884L * (long double)(i + 1) / (long double)(4 * n);
-        p->dtw[i] = (float)(double)cosl(ang);
-    }
+    for (int i = 0; i < n; ++i) p->dtw[i] = tw_cos(i + 1, 4 * n);
     p->norm = (float)(1.0L / sqrtl((long double)(2 * n)));
 }
 
 static void plans_init(void)
 {
     if (g_plans_ready) return;
-    plan_init(&g_plans[0], 4);
-    plan_init(&g_plans[1], 8);
-    plan_init(&g_plans[2], 16);
+    for (int k = 0; k < ORC_NPLANS; ++k) plan_init(&g_plans[k], 4 + 2 * k);
     g_plans_ready = 1;
 }
 
 static const dct_plan *plan_for(int n)
 {
     plans_init();
-    return n == 4 ? &g_plans[0] : n == 8 ? &g_plans[1] : &g_plans[2];
+    return &g_plans[(n - 4) / 2];
 }
 
 #define PM(a, b, c, d) do { float c_ = (c), d_ = (d); (a) = c_ + d_; (b) = c_ - d_; } while (0)
@@ -285,6 +301,155 @@ static void radf4(int ido, int l1, const float *cc, float *ch, const float *wa)
 #undef WA
 }
 
+/* Radix 3, 5 and generic (7) passes.  For every n <= 16 the odd factor is the last
+ * backward / first forward factor, so only their ido == 1 parts ever run; those
+ * parts are restated here (pocketfft radb3/radb5/radbg, radf3/radf5/radfg). */
+static const float TAUR = -0.5f, TAUI = 0.8660254037844386467637231707529362f;
+static const float TR11 = 0.3090169943749474241022934171828191f, TI11 = 0.9510565162951535721164393333793821f;
+static const float TR12 = -0.8090169943749474241022934171828191f, TI12 = 0.5877852522924731291687059546390728f;
+
+static void radb3(int l1, const float *cc, float *ch)
+{
+    for (int k = 0; k < l1; k++) {
+        const float tr2 = 2.0f * cc[1 + 3 * k];
+        const float cr2 = cc[3 * k] + TAUR * tr2;
+        ch[k] = cc[3 * k] + tr2;
+        const float ci3 = (2.0f * TAUI) * cc[2 + 3 * k];
+        PM(ch[k + 2 * l1], ch[k + l1], cr2, ci3);
+    }
+}
+
+static void radb5(int l1, const float *cc, float *ch)
+{
+    for (int k = 0; k < l1; k++) {
+        const float *c = cc + 5 * k;
+        const float ti5 = c[2] + c[2], ti4 = c[4] + c[4];
+        const float tr2 = c[1] + c[1], tr3 = c[3] + c[3];
+        ch[k] = c[0] + tr2 + tr3;
+        const float cr2 = c[0] + TR11 * tr2 + TR12 * tr3;
+        const float cr3 = c[0] + TR12 * tr2 + TR11 * tr3;
+        float ci4, ci5;
+        MULPM(ci5, ci4, ti5, ti4, TI11, TI12);
+        PM(ch[k + 4 * l1], ch[k + l1], cr2, ci5);
+        PM(ch[k + 3 * l1], ch[k + 2 * l1], cr3, ci4);
+    }
+}
+
+/* generic odd radix ip (7 for n = 14), ido == 1; csarr = plan tws.  cc is scratch. */
+static void radbg(int ip, int l1, float *cc, float *ch, const float *csarr)
+{
+    const int ipph = (ip + 1) / 2, idl1 = l1;
+#define RB_CC(b, c) cc[(b) + ip * (c)]
+#define RB_CH(b, c) ch[(b) + l1 * (c)]
+#define RB_C2(a, b) cc[(a) + idl1 * (b)]
+#define RB_CH2(a, b) ch[(a) + idl1 * (b)]
+    for (int k = 0; k < l1; ++k) RB_CH(k, 0) = RB_CC(0, k);
+    for (int j = 1, jc = ip - 1; j < ipph; ++j, --jc) {
+        const int j2 = 2 * j - 1;
+        for (int k = 0; k < l1; ++k) {
+            RB_CH(k, j) = 2.0f * RB_CC(j2, k);
+            RB_CH(k, jc) = 2.0f * RB_CC(j2 + 1, k);
+        }
+    }
+    for (int l = 1, lc = ip - 1; l < ipph; ++l, --lc) {
+        for (int ik = 0; ik < idl1; ++ik) {
+            RB_C2(ik, l) = RB_CH2(ik, 0) + csarr[2 * l] * RB_CH2(ik, 1) + csarr[4 * l] * RB_CH2(ik, 2);
+            RB_C2(ik, lc) = csarr[2 * l + 1] * RB_CH2(ik, ip - 1) + csarr[4 * l + 1] * RB_CH2(ik, ip - 2);
+        }
+        int iang = 2 * l;
+        for (int j = 3, jc = ip - 3; j < ipph; ++j, --jc) { /* ip <= 7: single-term tail only */
+            iang += l;
+            if (iang > ip) iang -= ip;
+            const float war = csarr[2 * iang], wai = csarr[2 * iang + 1];
+            for (int ik = 0; ik < idl1; ++ik) {
+                RB_C2(ik, l) += war * RB_CH2(ik, j);
+                RB_C2(ik, lc) += wai * RB_CH2(ik, jc);
+            }
+        }
+    }
+    for (int j = 1; j < ipph; ++j)
+        for (int ik = 0; ik < idl1; ++ik) RB_CH2(ik, 0) += RB_CH2(ik, j);
+    for (int j = 1, jc = ip - 1; j < ipph; ++j, --jc)
+        for (int k = 0; k < l1; ++k) PM(RB_CH(k, jc), RB_CH(k, j), RB_C2(k, j), RB_C2(k, jc));
+#undef RB_CC
+#undef RB_CH
+#undef RB_C2
+#undef RB_CH2
+}
+
+static void radf3(int l1, const float *cc, float *ch)
+{
+    for (int k = 0; k < l1; k++) {
+        const float cr2 = cc[k + l1] + cc[k + 2 * l1];
+        ch[3 * k] = cc[k] + cr2;
+        ch[2 + 3 * k] = TAUI * (cc[k + 2 * l1] - cc[k + l1]);
+        ch[1 + 3 * k] = cc[k] + TAUR * cr2;
+    }
+}
+
+static void radf5(int l1, const float *cc, float *ch)
+{
+    for (int k = 0; k < l1; k++) {
+        float cr2, cr3, ci4, ci5;
+        PM(cr2, ci5, cc[k + 4 * l1], cc[k + l1]);
+        PM(cr3, ci4, cc[k + 3 * l1], cc[k + 2 * l1]);
+        float *c = ch + 5 * k;
+        c[0] = cc[k] + cr2 + cr3;
+        c[1] = cc[k] + TR11 * cr2 + TR12 * cr3;
+        c[2] = TI11 * ci5 + TI12 * ci4;
+        c[3] = cc[k] + TR12 * cr2 + TR11 * cr3;
+        c[4] = TI12 * ci5 - TI11 * ci4;
+    }
+}
+
+/* generic odd radix, ido == 1; the result is left in cc (pocketfft swaps once more) */
+static void radfg(int ip, int l1, float *cc, float *ch, const float *csarr)
+{
+    const int ipph = (ip + 1) / 2, idl1 = l1;
+#define RF_CC(b, c) cc[(b) + ip * (c)]
+#define RF_CH(b, c) ch[(b) + l1 * (c)]
+#define RF_C1(b, c) cc[(b) + l1 * (c)]
+#define RF_C2(a, b) cc[(a) + idl1 * (b)]
+#define RF_CH2(a, b) ch[(a) + idl1 * (b)]
+    for (int j = 1, jc = ip - 1; j < ipph; ++j, --jc)
+        for (int k = 0; k < l1; ++k) {
+            const float t1 = RF_C1(k, j), t2 = RF_C1(k, jc);
+            PM(RF_C1(k, j), RF_C1(k, jc), t2, t1);
+        }
+    for (int l = 1, lc = ip - 1; l < ipph; ++l, --lc) {
+        for (int ik = 0; ik < idl1; ++ik) {
+            RF_CH2(ik, l) = RF_C2(ik, 0) + csarr[2 * l] * RF_C2(ik, 1) + csarr[4 * l] * RF_C2(ik, 2);
+            RF_CH2(ik, lc) = csarr[2 * l + 1] * RF_C2(ik, ip - 1) + csarr[4 * l + 1] * RF_C2(ik, ip - 2);
+        }
+        int iang = 2 * l;
+        for (int j = 3, jc = ip - 3; j < ipph; ++j, --jc) {
+            iang += l;
+            if (iang > ip) iang -= ip;
+            const float ar = csarr[2 * iang], ai = csarr[2 * iang + 1];
+            for (int ik = 0; ik < idl1; ++ik) {
+                RF_CH2(ik, l) += ar * RF_C2(ik, j);
+                RF_CH2(ik, lc) += ai * RF_C2(ik, jc);
+            }
+        }
+    }
+    for (int ik = 0; ik < idl1; ++ik) RF_CH2(ik, 0) = RF_C2(ik, 0);
+    for (int j = 1; j < ipph; ++j)
+        for (int ik = 0; ik < idl1; ++ik) RF_CH2(ik, 0) += RF_C2(ik, j);
+    for (int k = 0; k < l1; ++k) RF_CC(0, k) = RF_CH(k, 0);
+    for (int j = 1, jc = ip - 1; j < ipph; ++j, --jc) {
+        const int j2 = 2 * j - 1;
+        for (int k = 0; k < l1; ++k) {
+            RF_CC(j2, k) = RF_CH(k, j);
+            RF_CC(j2 + 1, k) = RF_CH(k, jc);
+        }
+    }
+#undef RF_CC
+#undef RF_CH
+#undef RF_C1
+#undef RF_C2
+#undef RF_CH2
+}
+
 /* rfftp::exec with copy_and_norm(fct) */
 static void rfft_exec(const dct_plan *p, float *c, float fct, int r2hc)
 {
@@ -296,14 +461,20 @@ static void rfft_exec(const dct_plan *p, float *c, float fct, int r2hc)
             int k = nf - k1 - 1, ip = p->fct[k], ido = n / l1;
             l1 /= ip;
             if (ip == 4) radf4(ido, l1, p1, p2, p->tw[k]);
-            else radf2(ido, l1, p1, p2, p->tw[k]);
+            else if (ip == 2) radf2(ido, l1, p1, p2, p->tw[k]);
+            else if (ip == 3) radf3(l1, p1, p2);
+            else if (ip == 5) radf5(l1, p1, p2);
+            else { radfg(ip, l1, p1, p2, p->tws[k]); float *t = p1; p1 = p2; p2 = t; }
             float *t = p1; p1 = p2; p2 = t;
         }
     } else {
         for (int k = 0, l1 = 1; k < nf; k++) {
             int ip = p->fct[k], ido = n / (ip * l1);
             if (ip == 4) radb4(ido, l1, p1, p2, p->tw[k]);
-            else radb2(ido, l1, p1, p2, p->tw[k]);
+            else if (ip == 2) radb2(ido, l1, p1, p2, p->tw[k]);
+            else if (ip == 3) radb3(l1, p1, p2);
+            else if (ip == 5) radb5(l1, p1, p2);
+            else radbg(ip, l1, p1, p2, p->tws[k]);
             float *t = p1; p1 = p2; p2 = t;
             l1 *= ip;
         }
@@ -379,10 +550,20 @@ static void dct2d(const dct_plan *p, float *blk, int inverse)
 #define JAC_TOL2 7.888609052210118e-31 /* 2^-100 */
 #define JAC_C2 9.860761315262648e-32   /* 2^-103 = 2 * (2^-52)^2 */
 
-/* Number of contiguous row chunks whose fma-chain partial sums are combined by a
- * balanced pairwise tree (matches the HIP layout: P lanes per block hold P row
- * chunks).  DESIGN.md 3.4. */
-static int jac_chunks(int b) { return b == 16 ? 8 : b == 8 ? 2 : 1; }
+/* Row chunks of the dot products: P chunks of R = ceil(b/P) contiguous rows (the
+ * last ones shorter or empty), their fma-chain partial sums combined by a balanced
+ * pairwise tree.  P is the number of GPU lanes per block (a power of two, so the
+ * xor butterfly realises the tree); empty chunks contribute +0, which leaves every
+ * sum unchanged.  DESIGN.md 3.4. */
+static int jac_chunks(int b)
+{
+    switch (b) {
+    case 4: return 1;
+    case 6: case 8: return 2;
+    case 10: case 12: return 4;
+    default: return 8; /* 14, 16 */
+    }
+}
 
 static double tree_sum(double *v, int n)
 {
@@ -396,11 +577,11 @@ static double tree_sum(double *v, int n)
 /* sum_r x[r*ldx] * y[r*ldy] in the contract order */
 static double cdot(const double *x, const double *y, int ld, int b)
 {
-    const int P = jac_chunks(b), R = b / P;
+    const int P = jac_chunks(b), R = (b + P - 1) / P;
     double part[ORC_MAXB];
     for (int q = 0; q < P; ++q) {
         double acc = 0.0;
-        for (int r = q * R; r < (q + 1) * R; ++r) acc = fma(x[r * ld], y[r * ld], acc);
+        for (int r = q * R; r < (q + 1) * R && r < b; ++r) acc = fma(x[r * ld], y[r * ld], acc);
         part[q] = acc;
     }
     return tree_sum(part, P);
@@ -504,11 +685,11 @@ static float tree_sumf(float *v, int n)
 /* f32 twin of cdot() (same chunks, fmaf chains, pairwise tree) */
 static float cdotf(const float *x, const float *y, int ld, int b)
 {
-    const int P = jac_chunks(b), R = b / P;
+    const int P = jac_chunks(b), R = (b + P - 1) / P;
     float part[ORC_MAXB];
     for (int q = 0; q < P; ++q) {
         float acc = 0.0f;
-        for (int r = q * R; r < (q + 1) * R; ++r) acc = fmaf(x[r * ld], y[r * ld], acc);
+        for (int r = q * R; r < (q + 1) * R && r < b; ++r) acc = fmaf(x[r * ld], y[r * ld], acc);
         part[q] = acc;
     }
     return tree_sumf(part, P);
@@ -723,7 +904,7 @@ void orc_blend_reconstruct_blocks(const float *U, const float *S, const float *V
 /* ------------------------------------------------------------------------ */
 /* Exported stage functions                                                 */
 /* ------------------------------------------------------------------------ */
-int orc_supported_block(int b) { return b == 4 || b == 8 || b == 16; }
+int orc_supported_block(int b) { return b >= 4 && b <= 16 && (b & 1) == 0; }
 
 void orc_rgb_to_ycbcr(const uint8_t *rgb, int64_t npix, float *ycc)
 {

@@ -27,6 +27,20 @@ def golden():
 
 
 @pytest.fixture(scope="session")
+def golden_blocks():
+    """Reference outputs for block sizes 6, 10, 12, 14 (gen_golden.py --blocks)."""
+    import json
+
+    import numpy as np
+
+    d = os.path.join(ROOT, "tests", "golden")
+    cases = np.load(os.path.join(d, "cases_blocks.npz"), allow_pickle=False)
+    with open(os.path.join(d, "meta_blocks.json")) as f:
+        meta = json.load(f)
+    return cases, meta
+
+
+@pytest.fixture(scope="session")
 def stages():
     import numpy as np
 

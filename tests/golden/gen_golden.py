@@ -16,7 +16,8 @@ Outputs (tests/golden/):
   meta.json        library versions, KAT hashes re-derived here,
                    per-case sha256 of every expected output
 
-Run:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py
+Run:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py            (cases.npz, stages.npz, meta.json)
+      PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py --blocks   (cases_blocks.npz, meta_blocks.json)
 """
 from __future__ import annotations
 
@@ -126,6 +127,23 @@ CASES = [
 ]
 
 
+# UI slider block sizes beyond 4/8/16 (embed_watermark_page.py:324-331): pocketfft
+# radix 3 (6, 12), 5 (10) and generic 7 (14).  Written to cases_blocks.npz /
+# meta_blocks.json by `gen_golden.py --blocks`, so the fixtures above stay as they are.
+BLOCK_CASES = [
+    ("noise_120x180_b6", "noise", 120, 180, "RGB", "noise", 20, 30, False, 6, 0.1, False),
+    ("diag_100x97_b6", "diagonal", 100, 97, "RGB", "pattern", 16, 16, False, 6, 0.15, False),
+    ("lmode_xor_96_b6", "xor", 96, 96, "L", "mul", 16, 16, False, 6, 0.1, False),
+    ("noise_125x173_b10_pr", "noise", 125, 173, "RGB", "qr", 21, 21, True, 10, 0.1, True),
+    ("smooth_150x200_b10", "smooth", 150, 200, "RGB", "noise", 15, 20, False, 10, 0.05, False),
+    ("noise_144x156_b12", "noise", 144, 156, "RGB", "noise", 12, 13, False, 12, 0.2, False),
+    ("blocky_120x130_b12", "blocky", 120, 130, "RGB", "noise", 10, 10, False, 12, 0.1, False),
+    ("noise_140x154_b14", "noise", 140, 154, "RGB", "noise", 10, 11, False, 14, 0.1, False),
+    ("rgba_112x126_b14", "noise", 112, 126, "RGBA", "pattern", 8, 9, False, 14, 0.15, False),
+    ("flat_84x84_b14", "flat", 84, 84, "RGB", "qr", 6, 6, False, 14, 0.1, False),
+]
+
+
 def _mode_img(arr: np.ndarray, mode: str):
     from PIL import Image
 
@@ -137,26 +155,14 @@ def _mode_img(arr: np.ndarray, mode: str):
     return Image.fromarray(arr, "RGB")
 
 
-def main() -> None:
+def run_cases(W, cases, seed_base: int, out: dict, meta: dict) -> None:
+    """embed_watermark / extract_watermark of the reference on every case."""
     from PIL import Image
 
-    W = _import_reference()
-    out: dict[str, np.ndarray] = {}
-    meta: dict = {
-        "generator": "tests/golden/gen_golden.py",
-        "reference": "/root/reference/modules/watermarking.py (embed_watermark :135, extract_watermark :224)",
-        "numpy": np.__version__,
-        "cases": {},
-    }
-    import PIL
-    import scipy
-
-    meta["scipy"] = scipy.__version__
-    meta["pillow"] = PIL.__version__
-    for seed, (name, ck, H, Wd, cmode, wk, wh, ww, as_bytes, b, alpha, pr) in enumerate(CASES):
-        carr = cover(ck, H, Wd, 1000 + seed)
+    for seed, (name, ck, H, Wd, cmode, wk, wh, ww, as_bytes, b, alpha, pr) in enumerate(cases):
+        carr = cover(ck, H, Wd, seed_base + seed)
         cimg = _mode_img(carr, cmode)
-        warr = wmark(wk, wh, ww, 2000 + seed)
+        warr = wmark(wk, wh, ww, seed_base + 1000 + seed)
         wimg = Image.fromarray(warr, "L")
         if as_bytes:
             buf = io.BytesIO()
@@ -182,6 +188,42 @@ def main() -> None:
             "sha_embed": sha(e_arr), "sha_extract": sha(x_arr), "sha_tile": sha(t_arr),
         }
         print(name, cimg.mode, e_arr.shape, x_arr.shape, flush=True)
+
+
+def main_blocks() -> None:
+    """cases_blocks.npz + meta_blocks.json: block sizes 6, 10, 12, 14."""
+    import PIL
+    import scipy
+
+    W = _import_reference()
+    out: dict[str, np.ndarray] = {}
+    meta: dict = {"generator": "tests/golden/gen_golden.py --blocks",
+                  "reference": "/root/reference/modules/watermarking.py (embed_watermark :135, extract_watermark :224)",
+                  "numpy": np.__version__, "scipy": scipy.__version__, "pillow": PIL.__version__, "cases": {}}
+    run_cases(W, BLOCK_CASES, 3000, out, meta)
+    np.savez_compressed(os.path.join(HERE, "cases_blocks.npz"), **out)
+    with open(os.path.join(HERE, "meta_blocks.json"), "w") as f:
+        json.dump(meta, f, indent=1, sort_keys=True)
+    print("wrote cases_blocks.npz, meta_blocks.json")
+
+
+def main() -> None:
+    from PIL import Image
+
+    W = _import_reference()
+    out: dict[str, np.ndarray] = {}
+    meta: dict = {
+        "generator": "tests/golden/gen_golden.py",
+        "reference": "/root/reference/modules/watermarking.py (embed_watermark :135, extract_watermark :224)",
+        "numpy": np.__version__,
+        "cases": {},
+    }
+    import PIL
+    import scipy
+
+    meta["scipy"] = scipy.__version__
+    meta["pillow"] = PIL.__version__
+    run_cases(W, CASES, 1000, out, meta)
 
     # ---- per-stage intermediates on one noise cover (watermarking.py:166-216)
     carr = cover("noise", 64, 48, 77)
@@ -234,4 +276,7 @@ def main() -> None:
 
 
 if __name__ == "__main__":
-    main()
+    if "--blocks" in sys.argv[1:]:
+        main_blocks()
+    else:
+        main()
