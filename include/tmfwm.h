@@ -22,8 +22,8 @@
  * Image layout: n_frames frames of height x width x 3 uint8, HWC interleaved
  * (numpy / PIL "RGB" order), frame i at base + i * frame_stride bytes
  * (frame_stride >= height*width*3).  Block grid: nbh = height / block,
- * nbw = width / block.  Supported block sizes: 4, 8, 16 (others return
- * TMFWM_ERR_UNSUPPORTED).
+ * nbw = width / block.  Supported block sizes: 4, 6, 8, 10, 12, 14, 16 -- the app's
+ * slider values (others return TMFWM_ERR_UNSUPPORTED).
  */
 #ifndef TMFWM_H
 #define TMFWM_H

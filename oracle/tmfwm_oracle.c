@@ -95,12 +95,53 @@ typedef struct {
 static dct_plan g_plans[ORC_NPLANS];
 static int g_plans_ready = 0;
 
-static const long double ORC_PI = 3.141592653589793238462643383279502884L;
+static const long double ORC_PI = 3.141592653589793238462643383279502884197L;
 
-/* comp_twiddle's twid[m] = (cos 2 pi m / n, sin 2 pi m / n): pocketfft's sincos_2pibyn
- * computes them in double for a float plan and rounds; long double here, same floats */
-static float tw_cos(long m, long n) { return (float)(double)cosl(2.0L * ORC_PI * (long double)m / (long double)n); }
-static float tw_sin(long m, long n) { return (float)(double)sinl(2.0L * ORC_PI * (long double)m / (long double)n); }
+/* twid[m] = (cos, sin)(2 pi m / n) exactly as pocketfft's sincos_2pibyn<float> makes
+ * them: octant-reduced cos/sin in double on a two-level (v1[m & mask], v2[m >> shift])
+ * table, complex product in double, rounded to float.  Exact-quadrant angles come
+ * out as exact signed zeros (cos(2 pi 3/12) = -0.0f), which the N = 12 radix-4 pass
+ * uses; a plain cos() would give -2.5e-20f there. */
+typedef struct { double r, i; } orc_cd;
+static orc_cd sc_calc(size_t x, size_t n, double ang)
+{
+    orc_cd o;
+    x <<= 3;
+    if (x < 4 * n) {
+        if (x < 2 * n) {
+            if (x < n) { o.r = cos((double)x * ang); o.i = sin((double)x * ang); return o; }
+            o.r = sin((double)(2 * n - x) * ang); o.i = cos((double)(2 * n - x) * ang); return o;
+        }
+        x -= 2 * n;
+        if (x < n) { o.r = -sin((double)x * ang); o.i = cos((double)x * ang); return o; }
+        o.r = -cos((double)(2 * n - x) * ang); o.i = sin((double)(2 * n - x) * ang); return o;
+    }
+    x = 8 * n - x;
+    if (x < 2 * n) {
+        if (x < n) { o.r = cos((double)x * ang); o.i = -sin((double)x * ang); return o; }
+        o.r = sin((double)(2 * n - x) * ang); o.i = -cos((double)(2 * n - x) * ang); return o;
+    }
+    x -= 4 * n;
+    if (x < n) { o.r = -sin((double)x * ang); o.i = -cos((double)x * ang); return o; }
+    o.r = -cos((double)(2 * n - x) * ang); o.i = -sin((double)(2 * n - x) * ang); return o;
+}
+static void sincos_2pibyn(size_t n, size_t idx, float *re, float *im)
+{
+    const double ang = (double)(0.25L * ORC_PI / (long double)n);
+    size_t nval = (n + 2) / 2, shift = 1;
+    while (((size_t)1 << shift) * ((size_t)1 << shift) < nval) ++shift;
+    const size_t mask = ((size_t)1 << shift) - 1;
+    int conj = 0;
+    if (!(2 * idx <= n)) { idx = n - idx; conj = 1; }
+    const orc_cd one = {1.0, 0.0};
+    const orc_cd x1 = (idx & mask) ? sc_calc(idx & mask, n, ang) : one;
+    const orc_cd x2 = (idx >> shift) ? sc_calc((idx >> shift) * (mask + 1), n, ang) : one;
+    *re = (float)(x1.r * x2.r - x1.i * x2.i);
+    const float i = (float)(x1.r * x2.i + x1.i * x2.r);
+    *im = conj ? -i : i;
+}
+static float tw_cos(long m, long n) { float r, i; sincos_2pibyn((size_t)n, (size_t)m, &r, &i); return r; }
+static float tw_sin(long m, long n) { float r, i; sincos_2pibyn((size_t)n, (size_t)m, &r, &i); return i; }
 
 static void plan_init(dct_plan *p, int n)
 {

@@ -48,8 +48,9 @@ def test_argument_validation_before_device():
     t = np.zeros((2, 2), np.uint8)
     o = np.empty_like(a)
     p = lambda x: x.ctypes.data  # noqa: E731
-    with pytest.raises(NotImplementedError):  # block 6 (UI slider value) is not supported
-        _lib.check(L.tmfwm_embed(p(a), 1, 16, 16, a.size, p(t), 6, 0.1, p(o), _lib.MEM_HOST, None), "embed")
+    for bad_block in (7, 18, 2):  # the app's slider offers 4..16 step 2; nothing else is supported
+        with pytest.raises(NotImplementedError):
+            _lib.check(L.tmfwm_embed(p(a), 1, 16, 16, a.size, p(t), bad_block, 0.1, p(o), _lib.MEM_HOST, None), "embed")
     with pytest.raises(ValueError):  # negative size
         _lib.check(L.tmfwm_embed(p(a), -1, 16, 16, a.size, p(t), 8, 0.1, p(o), _lib.MEM_HOST, None), "embed")
     with pytest.raises(ValueError):  # frame stride shorter than a frame

@@ -50,13 +50,17 @@ def test_colour_tables_exhaustive_gpu(dev, golden):
     assert sha(W.ycbcr_to_rgb(ycc)) == meta["kats"]["colour_roundtrip_table_sha256"]
 
 
-@pytest.mark.parametrize("b", [4, 8, 16])
+ALL_B = [4, 6, 8, 10, 12, 14, 16]  # the app's block-size slider (embed_watermark_page.py:324-331)
+
+
+@pytest.mark.parametrize("b", ALL_B)
 def test_dct_blocks_gpu(dev, b):
     from thatsmyface_amd import watermarking as W
 
     rng = np.random.default_rng(b)
     x = np.concatenate([rng.random((4000, b, b), dtype=np.float32),
-                        (rng.standard_normal((1000, b, b)) * 1e-3).astype(np.float32)])
+                        (rng.standard_normal((1000, b, b)) * 1e-3).astype(np.float32),
+                        rng.integers(0, 3, (500, b, b)).astype(np.float32), np.ones((1, b, b), np.float32)])
     d = W.apply_dct_to_block(x)
     assert np.array_equal(d.view(np.uint32), O.dct2d_blocks(x).view(np.uint32))
     i = W.apply_idct_to_block(x)
@@ -73,7 +77,7 @@ def _svd_corpus(b):
     return np.concatenate(out)
 
 
-@pytest.mark.parametrize("b", [4, 8, 16])
+@pytest.mark.parametrize("b", ALL_B)
 def test_svd_blocks_gpu_bit_identical(dev, b):
     from thatsmyface_amd import batch
 
@@ -120,6 +124,21 @@ def test_golden_cases_dropin_gpu(dev, golden):
         assert np.array_equal(np.asarray(ex), cases[f"{name}/extract"]), name
 
 
+def test_golden_block_sizes_dropin_gpu(dev, golden_blocks):
+    """Block sizes 6, 10, 12, 14 through the drop-in API against the reference's bytes."""
+    from thatsmyface_amd import watermarking as W
+
+    cases, meta = golden_blocks
+    for name, m in meta["cases"].items():
+        cov = _cover_image(cases[f"{name}/cover"])
+        wm = Image.fromarray(cases[f"{name}/wm"], "L")
+        settings = {"block_size": m["block"], "alpha": m["alpha"]}
+        e = np.asarray(W.embed_watermark(cov, wm, m["preserve_ratio"], settings))
+        assert np.array_equal(e, cases[f"{name}/embed"]), name
+        ex = W.extract_watermark(Image.fromarray(cases[f"{name}/embed"]), cov, settings)
+        assert np.array_equal(np.asarray(ex), cases[f"{name}/extract"]), name
+
+
 def test_golden_png_bytes_watermark_gpu(dev, golden):
     """watermark_data as PNG bytes (the app's call site, embed_watermark_page.py:529-531)."""
     import io
@@ -149,7 +168,9 @@ def test_stages_gpu(dev, stages):
 
 # ---------------------------------------------------------------- batches in HBM vs the oracle
 @pytest.mark.parametrize("b,h,w,n", [(8, 1080, 1920, 2), (8, 250, 333, 3), (16, 1088, 1920, 1), (4, 131, 258, 2),
-                                     (16, 200, 170, 2), (8, 2160, 3840, 1)])
+                                     (16, 200, 170, 2), (8, 2160, 3840, 1), (6, 1080, 1920, 1), (10, 1080, 1920, 1),
+                                     (12, 1080, 1920, 1), (14, 1080, 1920, 1), (6, 133, 251, 2), (10, 157, 263, 2),
+                                     (12, 149, 301, 2), (14, 211, 167, 2)])
 def test_batch_embed_extract_vs_oracle(dev, b, h, w, n):
     from thatsmyface_amd import batch
 
@@ -173,7 +194,7 @@ def test_batch_structured_covers_vs_oracle(dev):
 
     from thatsmyface_amd import batch
 
-    for b in (4, 8, 16):
+    for b in ALL_B:
         for kind in ("qr", "black", "flat", "smooth", "blocky", "diagonal"):
             c = np.ascontiguousarray(cover(kind, 256, 320, 11))
             t = wmark("qr", 256 // b, 320 // b, 12)
@@ -184,11 +205,12 @@ def test_batch_structured_covers_vs_oracle(dev):
             assert np.array_equal(ext[0].cpu().numpy(), O.extract_frame(ref, c, b, 0.15)), (b, kind)
 
 
-def test_unaligned_strided_frames(dev):
+@pytest.mark.parametrize("b", [8, 6, 12, 14])
+def test_unaligned_strided_frames(dev, b):
     """Frames at odd byte offsets / strides take the byte-granular load path."""
     from thatsmyface_amd import _lib
 
-    h, w, b = 64, 72, 8
+    h, w = 64 + b // 2, 72 + b
     raw = _u8(5, (3 * h * w * 3 + 7,))
     stride = h * w * 3 + 1
     src = torch.from_numpy(raw).to(dev)
@@ -245,5 +267,5 @@ def test_empty_and_degenerate(dev):
         _lib.check(_lib.load().tmfwm_embed(h.ctypes.data, 1, 8, 8, 192, h.ctypes.data, 8, 0.1, h.ctypes.data,
                                            _lib.MEM_DEVICE, None), "embed")
     with pytest.raises(NotImplementedError):
-        batch.embed_batch(torch.zeros((1, 12, 12, 3), dtype=torch.uint8, device=dev),
-                          torch.zeros((2, 2), dtype=torch.uint8, device=dev), 6, 0.1)
+        batch.embed_batch(torch.zeros((1, 14, 14, 3), dtype=torch.uint8, device=dev),
+                          torch.zeros((2, 2), dtype=torch.uint8, device=dev), 7, 0.1)

@@ -34,7 +34,7 @@ int fail(int code, const char *fmt, ...)
 
 hipStream_t pick_stream(void *s) { return s ? reinterpret_cast<hipStream_t>(s) : hipStreamPerThread; }
 
-bool supported_block(int b) { return b == 4 || b == 8 || b == 16; }
+bool supported_block(int b) { return b >= 4 && b <= 16 && b % 2 == 0; }  // the UI slider values
 
 // A device pointer handed in as TMFWM_MEM_DEVICE must really be device memory:
 // a host pointer dereferenced by a kernel would fault the GPU.
@@ -77,7 +77,7 @@ struct DevBuf {
 int check_frames(int64_t n, int32_t H, int32_t W, int64_t stride, int32_t block)
 {
     if (n < 0 || H < 0 || W < 0) return fail(TMFWM_ERR_INVALID, "negative size (n=%lld, H=%d, W=%d)", (long long)n, H, W);
-    if (!supported_block(block)) return fail(TMFWM_ERR_UNSUPPORTED, "block size %d not supported (4, 8, 16)", block);
+    if (!supported_block(block)) return fail(TMFWM_ERR_UNSUPPORTED, "block size %d not supported (even, 4..16)", block);
     if (stride < (int64_t)H * W * 3) return fail(TMFWM_ERR_INVALID, "frame_stride %lld < H*W*3", (long long)stride);
     return 0;
 }

@@ -67,7 +67,7 @@ TMF_DEVI void colour_inv(float y, float cbs, float crs, uint32_t &R, uint32_t &G
 }
 
 // ---------------------------------------------------------------------------
-// pocketfft fp32 DCT-II / DCT-III (N3), lengths 4, 8, 16, fully unrolled on
+// pocketfft fp32 DCT-II / DCT-III (N3), every even length 4..16, fully unrolled on
 // register arrays.  rfftp radix passes with compile-time (ido, l1).
 // ---------------------------------------------------------------------------
 namespace dct {
@@ -282,8 +282,186 @@ TMF_DEVI void radf4(const float (&cc)[N], float (&ch)[N], const float *wa)
 #undef CH
 }
 
-// rfftp::exec for the factorisations pocketfft picks: 4 -> [4], 8 -> [2,4], 16 -> [4,4];
-// copy_and_norm multiplies by fct at the end.
+// Radix 3, 5 and generic odd (7) passes.  For N <= 16 the odd factor is always the
+// last backward / first forward factor, so only their ido == 1 parts exist
+// (oracle radb3/radb5/radbg, radf3/radf5/radfg).
+constexpr float kTaur = -0.5f, kTaui = 0.8660254037844386467637231707529362f;
+constexpr float kTr11 = 0.3090169943749474241022934171828191f, kTi11 = 0.9510565162951535721164393333793821f;
+constexpr float kTr12 = -0.8090169943749474241022934171828191f, kTi12 = 0.5877852522924731291687059546390728f;
+
+template <int L1, int N>
+TMF_DEVI void radb3(const float (&cc)[N], float (&ch)[N])
+{
+#pragma unroll
+    for (int k = 0; k < L1; k++) {
+        const float tr2 = 2.0f * cc[1 + 3 * k];
+        const float cr2 = cc[3 * k] + kTaur * tr2;
+        ch[k] = cc[3 * k] + tr2;
+        const float ci3 = (2.0f * kTaui) * cc[2 + 3 * k];
+        ch[k + 2 * L1] = cr2 + ci3;
+        ch[k + L1] = cr2 - ci3;
+    }
+}
+
+template <int L1, int N>
+TMF_DEVI void radb5(const float (&cc)[N], float (&ch)[N])
+{
+#pragma unroll
+    for (int k = 0; k < L1; k++) {
+        const float c0 = cc[5 * k], c1 = cc[5 * k + 1], c2 = cc[5 * k + 2], c3 = cc[5 * k + 3], c4 = cc[5 * k + 4];
+        const float ti5 = c2 + c2, ti4 = c4 + c4, tr2 = c1 + c1, tr3 = c3 + c3;
+        ch[k] = c0 + tr2 + tr3;
+        const float cr2 = c0 + kTr11 * tr2 + kTr12 * tr3;
+        const float cr3 = c0 + kTr12 * tr2 + kTr11 * tr3;
+        const float ci5 = ti5 * kTi11 + ti4 * kTi12, ci4 = ti5 * kTi12 - ti4 * kTi11;
+        ch[k + 4 * L1] = cr2 + ci5;
+        ch[k + L1] = cr2 - ci5;
+        ch[k + 3 * L1] = cr3 + ci4;
+        ch[k + 2 * L1] = cr3 - ci4;
+    }
+}
+
+// generic odd radix IP <= 7 (single-term tail of pocketfft's accumulation), ido == 1;
+// cc is scratch, the result is in ch
+template <int IP, int L1, int N>
+TMF_DEVI void radbg(float (&cc)[N], float (&ch)[N], const float *cs)
+{
+    static_assert(IP <= 7, "accumulation tail restated for ip <= 7 only");
+    constexpr int IPPH = (IP + 1) / 2;
+#pragma unroll
+    for (int k = 0; k < L1; ++k) ch[k] = cc[IP * k];
+#pragma unroll
+    for (int j = 1; j < IPPH; ++j) {
+        const int jc = IP - j, j2 = 2 * j - 1;
+#pragma unroll
+        for (int k = 0; k < L1; ++k) {
+            ch[k + L1 * j] = 2.0f * cc[j2 + IP * k];
+            ch[k + L1 * jc] = 2.0f * cc[j2 + 1 + IP * k];
+        }
+    }
+#pragma unroll
+    for (int l = 1; l < IPPH; ++l) {
+        const int lc = IP - l;
+#pragma unroll
+        for (int ik = 0; ik < L1; ++ik) {
+            cc[ik + L1 * l] = ch[ik] + cs[2 * l] * ch[ik + L1] + cs[4 * l] * ch[ik + 2 * L1];
+            cc[ik + L1 * lc] = cs[2 * l + 1] * ch[ik + L1 * (IP - 1)] + cs[4 * l + 1] * ch[ik + L1 * (IP - 2)];
+        }
+        int iang = 2 * l;
+#pragma unroll
+        for (int j = 3; j < IPPH; ++j) {
+            const int jc = IP - j;
+            iang += l;
+            if (iang > IP) iang -= IP;
+#pragma unroll
+            for (int ik = 0; ik < L1; ++ik) {
+                cc[ik + L1 * l] = cc[ik + L1 * l] + cs[2 * iang] * ch[ik + L1 * j];
+                cc[ik + L1 * lc] = cc[ik + L1 * lc] + cs[2 * iang + 1] * ch[ik + L1 * jc];
+            }
+        }
+    }
+#pragma unroll
+    for (int j = 1; j < IPPH; ++j)
+#pragma unroll
+        for (int ik = 0; ik < L1; ++ik) ch[ik] = ch[ik] + ch[ik + L1 * j];
+#pragma unroll
+    for (int j = 1; j < IPPH; ++j) {
+        const int jc = IP - j;
+#pragma unroll
+        for (int k = 0; k < L1; ++k) {
+            const float a = cc[k + L1 * j], b = cc[k + L1 * jc];
+            ch[k + L1 * jc] = a + b;
+            ch[k + L1 * j] = a - b;
+        }
+    }
+}
+
+template <int L1, int N>
+TMF_DEVI void radf3(const float (&cc)[N], float (&ch)[N])
+{
+#pragma unroll
+    for (int k = 0; k < L1; k++) {
+        const float cr2 = cc[k + L1] + cc[k + 2 * L1];
+        ch[3 * k] = cc[k] + cr2;
+        ch[2 + 3 * k] = kTaui * (cc[k + 2 * L1] - cc[k + L1]);
+        ch[1 + 3 * k] = cc[k] + kTaur * cr2;
+    }
+}
+
+template <int L1, int N>
+TMF_DEVI void radf5(const float (&cc)[N], float (&ch)[N])
+{
+#pragma unroll
+    for (int k = 0; k < L1; k++) {
+        const float cr2 = cc[k + 4 * L1] + cc[k + L1], ci5 = cc[k + 4 * L1] - cc[k + L1];
+        const float cr3 = cc[k + 3 * L1] + cc[k + 2 * L1], ci4 = cc[k + 3 * L1] - cc[k + 2 * L1];
+        ch[5 * k] = cc[k] + cr2 + cr3;
+        ch[5 * k + 1] = cc[k] + kTr11 * cr2 + kTr12 * cr3;
+        ch[5 * k + 2] = kTi11 * ci5 + kTi12 * ci4;
+        ch[5 * k + 3] = cc[k] + kTr12 * cr2 + kTr11 * cr3;
+        ch[5 * k + 4] = kTi12 * ci5 - kTi11 * ci4;
+    }
+}
+
+// generic odd radix, ido == 1: the result is left in cc (ch is scratch)
+template <int IP, int L1, int N>
+TMF_DEVI void radfg(float (&cc)[N], float (&ch)[N], const float *cs)
+{
+    static_assert(IP <= 7, "accumulation tail restated for ip <= 7 only");
+    constexpr int IPPH = (IP + 1) / 2;
+#pragma unroll
+    for (int j = 1; j < IPPH; ++j) {
+        const int jc = IP - j;
+#pragma unroll
+        for (int k = 0; k < L1; ++k) {
+            const float t1 = cc[k + L1 * j], t2 = cc[k + L1 * jc];
+            cc[k + L1 * j] = t2 + t1;
+            cc[k + L1 * jc] = t2 - t1;
+        }
+    }
+#pragma unroll
+    for (int l = 1; l < IPPH; ++l) {
+        const int lc = IP - l;
+#pragma unroll
+        for (int ik = 0; ik < L1; ++ik) {
+            ch[ik + L1 * l] = cc[ik] + cs[2 * l] * cc[ik + L1] + cs[4 * l] * cc[ik + 2 * L1];
+            ch[ik + L1 * lc] = cs[2 * l + 1] * cc[ik + L1 * (IP - 1)] + cs[4 * l + 1] * cc[ik + L1 * (IP - 2)];
+        }
+        int iang = 2 * l;
+#pragma unroll
+        for (int j = 3; j < IPPH; ++j) {
+            const int jc = IP - j;
+            iang += l;
+            if (iang > IP) iang -= IP;
+#pragma unroll
+            for (int ik = 0; ik < L1; ++ik) {
+                ch[ik + L1 * l] = ch[ik + L1 * l] + cs[2 * iang] * cc[ik + L1 * j];
+                ch[ik + L1 * lc] = ch[ik + L1 * lc] + cs[2 * iang + 1] * cc[ik + L1 * jc];
+            }
+        }
+    }
+#pragma unroll
+    for (int ik = 0; ik < L1; ++ik) ch[ik] = cc[ik];
+#pragma unroll
+    for (int j = 1; j < IPPH; ++j)
+#pragma unroll
+        for (int ik = 0; ik < L1; ++ik) ch[ik] = ch[ik] + cc[ik + L1 * j];
+#pragma unroll
+    for (int k = 0; k < L1; ++k) cc[IP * k] = ch[k];
+#pragma unroll
+    for (int j = 1; j < IPPH; ++j) {
+        const int jc = IP - j, j2 = 2 * j - 1;
+#pragma unroll
+        for (int k = 0; k < L1; ++k) {
+            cc[j2 + IP * k] = ch[k + L1 * j];
+            cc[j2 + 1 + IP * k] = ch[k + L1 * jc];
+        }
+    }
+}
+
+// rfftp::exec for the factorisations pocketfft picks (4 -> [4], 6 -> [2,3],
+// 8 -> [2,4], 10 -> [2,5], 12 -> [4,3], 14 -> [2,7], 16 -> [4,4]); copy_and_norm
+// multiplies by fct at the end.
 template <int N>
 TMF_DEVI void rfft_backward(float (&c)[N], float fct)
 {
@@ -292,17 +470,28 @@ TMF_DEVI void rfft_backward(float (&c)[N], float fct)
         radb4<1, 1>(c, ch, nullptr);
 #pragma unroll
         for (int i = 0; i < N; ++i) c[i] = fct * ch[i];
+        return;
+    } else if constexpr (N == 6) {
+        radb2<3, 1>(c, ch, kRfftTw6);
+        radb3<2>(ch, c);
     } else if constexpr (N == 8) {
         radb2<4, 1>(c, ch, kRfftTw8);
         radb4<1, 2>(ch, c, nullptr);
-#pragma unroll
-        for (int i = 0; i < N; ++i) c[i] *= fct;
+    } else if constexpr (N == 10) {
+        radb2<5, 1>(c, ch, kRfftTw10);
+        radb5<2>(ch, c);
+    } else if constexpr (N == 12) {
+        radb4<3, 1>(c, ch, kRfftTw12);
+        radb3<4>(ch, c);
+    } else if constexpr (N == 14) {
+        radb2<7, 1>(c, ch, kRfftTw14);
+        radbg<7, 2>(ch, c, kRfftTws14);
     } else {
         radb4<4, 1>(c, ch, kRfftTw16);
         radb4<1, 4>(ch, c, nullptr);
-#pragma unroll
-        for (int i = 0; i < N; ++i) c[i] *= fct;
     }
+#pragma unroll
+    for (int i = 0; i < N; ++i) c[i] *= fct;
 }
 
 template <int N>
@@ -313,23 +502,43 @@ TMF_DEVI void rfft_forward(float (&c)[N], float fct)
         radf4<1, 1>(c, ch, nullptr);
 #pragma unroll
         for (int i = 0; i < N; ++i) c[i] = fct * ch[i];
+        return;
+    } else if constexpr (N == 6) {
+        radf3<2>(c, ch);
+        radf2<3, 1>(ch, c, kRfftTw6);
     } else if constexpr (N == 8) {
         radf4<1, 2>(c, ch, nullptr);
         radf2<4, 1>(ch, c, kRfftTw8);
+    } else if constexpr (N == 10) {
+        radf5<2>(c, ch);
+        radf2<5, 1>(ch, c, kRfftTw10);
+    } else if constexpr (N == 12) {
+        radf3<4>(c, ch);
+        radf4<3, 1>(ch, c, kRfftTw12);
+    } else if constexpr (N == 14) {
+        radfg<7, 2>(c, ch, kRfftTws14);  // result stays in c
+        radf2<7, 1>(c, ch, kRfftTw14);
 #pragma unroll
-        for (int i = 0; i < N; ++i) c[i] *= fct;
+        for (int i = 0; i < N; ++i) c[i] = fct * ch[i];
+        return;
     } else {
         radf4<1, 4>(c, ch, nullptr);
         radf4<4, 1>(ch, c, kRfftTw16);
-#pragma unroll
-        for (int i = 0; i < N; ++i) c[i] *= fct;
     }
+#pragma unroll
+    for (int i = 0; i < N; ++i) c[i] *= fct;
 }
 
 template <int N> struct Tw;
-template <> struct Tw<4> { static constexpr const float *d = kDctTw4; static constexpr float norm = kNorm4; };
-template <> struct Tw<8> { static constexpr const float *d = kDctTw8; static constexpr float norm = kNorm8; };
-template <> struct Tw<16> { static constexpr const float *d = kDctTw16; static constexpr float norm = kNorm16; };
+#define TMF_TW(N) template <> struct Tw<N> { static constexpr const float *d = kDctTw##N; static constexpr float norm = kNorm##N; }
+TMF_TW(4);
+TMF_TW(6);
+TMF_TW(8);
+TMF_TW(10);
+TMF_TW(12);
+TMF_TW(14);
+TMF_TW(16);
+#undef TMF_TW
 
 // T_dcst23 type 2 (scipy.fftpack.dct, norm="ortho")
 template <int N>
@@ -587,12 +796,17 @@ TMF_DEVI Rot<T> rotation(T alpha, T beta, T gamma)
 // no block of the wave rotates costs nothing, and inside the branch lanes whose
 // block skips it apply the bitwise-exact identity (no divergent exec masks, so
 // the updates stay in place instead of being computed aside and copied back).
+// Rows per lane: ceil(B / L); rows past B are zero padding (exact: they add +0 to
+// every dot product and stay 0 under every rotation).
+template <int B, int L>
+constexpr int kRows = (B + L - 1) / L;
+
 template <typename T, int B, int L, bool WANT_V>
-TMF_DEVI int jacobi(T (&A)[B / L][B], T (&V)[B / L][B], int q)
+TMF_DEVI int jacobi(T (&A)[(B + L - 1) / L][B], T (&V)[(B + L - 1) / L][B], int q)
 {
     using P = JacP<T>;
-    constexpr int R = B / L, NP = B / 2, PP = NP / L;
-    static_assert(PP >= 1, "need L <= B/2");
+    // NP pairs per round; lane q evaluates pairs [q*PP, q*PP + PP) that exist
+    constexpr int R = kRows<B, L>, NP = B / 2, PP = (NP + L - 1) / L;
     T F = T(0);
     static_for<B>([&](auto K) { F += cdot<R, B, L>(A, K, K); });
     const T c2 = P::kC2 * F;
@@ -627,13 +841,18 @@ TMF_DEVI int jacobi(T (&A)[B / L][B], T (&V)[B / L][B], int q)
                 T a = nrm[i0], b = nrm[j0], g = ga[p0];
                 bool o = on[p0];
                 static_for<L - 1>([&](auto Q1) {
-                    constexpr int QQ = Q1 + 1, p = QQ * PP + U, i = Sched<B>::lo(s, p), j = Sched<B>::hi(s, p);
+                    constexpr int QQ = Q1 + 1, p = QQ * PP + U;
                     int m = -(int)(q == QQ);
                     asm volatile("" : "+v"(m));
-                    a = blend(m, nrm[i], a);
-                    b = blend(m, nrm[j], b);
-                    g = blend(m, ga[p], g);
-                    o = (m & (int)on[p]) | (~m & (int)o);
+                    if constexpr (p < NP) {
+                        constexpr int i = Sched<B>::lo(s, p), j = Sched<B>::hi(s, p);
+                        a = blend(m, nrm[i], a);
+                        b = blend(m, nrm[j], b);
+                        g = blend(m, ga[p], g);
+                        o = (m & (int)on[p]) | (~m & (int)o);
+                    } else {
+                        o = ~m & (int)o;  // lane QQ has no U-th pair this round
+                    }
                 });
                 mine[U] = Rot<T>{T(1), T(0), T(0)};
                 if (!P::kBranchy || __any(o)) {  // wave-uniform: every lane computes, non-rotating lanes keep identity
@@ -683,9 +902,9 @@ TMF_DEVI int jacobi(T (&A)[B / L][B], T (&V)[B / L][B], int q)
 // Phase 2 (oracle bjorck()): V <- V N, N = 1.5 I - 0.5 V^T V.  N is symmetric and
 // cdot(V, j, k) == cdot(V, k, j) bitwise, so only the upper triangle is computed.
 template <int B, int L>
-TMF_DEVI void bjorck(double (&V)[B / L][B])
+TMF_DEVI void bjorck(double (&V)[(B + L - 1) / L][B])
 {
-    constexpr int R = B / L;
+    constexpr int R = kRows<B, L>;
     if constexpr (B > 8) {  // 136 packed doubles would not fit in registers: column by column
         double T[R][B];
         static_for<B>([&](auto K) {
@@ -740,9 +959,9 @@ TMF_DEVI void bjorck(double (&V)[B / L][B])
 
 // A0 = D V (oracle: fma chain over j = 0..b-1); row j of V comes from lane j / R.
 template <int B, int L>
-TMF_DEVI void mul_dv(const float (&D)[B / L][B], const double (&V)[B / L][B], double (&A)[B / L][B])
+TMF_DEVI void mul_dv(const float (&D)[(B + L - 1) / L][B], const double (&V)[(B + L - 1) / L][B], double (&A)[(B + L - 1) / L][B])
 {
-    constexpr int R = B / L;
+    constexpr int R = kRows<B, L>;
 #pragma unroll
     for (int r = 0; r < R; ++r)
 #pragma unroll
@@ -767,9 +986,10 @@ struct NoStamp {
 };
 
 template <int B, int L, typename Stamp = NoStamp>
-TMF_DEVI int svd3(const float (&D)[B / L][B], double (&A)[B / L][B], double (&V)[B / L][B], int q, Stamp stamp = {})
+TMF_DEVI int svd3(const float (&D)[(B + L - 1) / L][B], double (&A)[(B + L - 1) / L][B], double (&V)[(B + L - 1) / L][B], int q,
+                  Stamp stamp = {})
 {
-    constexpr int R = B / L;
+    constexpr int R = kRows<B, L>;
     int s32;
     {
         float A32[R][B], V32[R][B];
@@ -808,9 +1028,9 @@ TMF_DEVI int svd3(const float (&D)[B / L][B], double (&A)[B / L][B], double (&V)
 // reference; otherwise the caller falls back to the exact Jacobi.
 // ---------------------------------------------------------------------------
 template <int B, int L, int ITERS>
-TMF_DEVI bool sigma1_certified(const float (&x)[B / L][B], float &s1)
+TMF_DEVI bool sigma1_certified(const float (&x)[(B + L - 1) / L][B], float &s1)
 {
-    constexpr int R = B / L;
+    constexpr int R = kRows<B, L>;
     constexpr double u = 1.1102230246251565e-16;  // 2^-53
     float v[B];
 #pragma unroll

@@ -36,45 +36,55 @@ using Stamp = NoStamp;
 #define TMF_STAMP_INIT const Stamp stamp{}
 #endif
 
+// Lanes per block L (== oracle jac_chunks): a power of two for the DPP butterflies,
+// with R = ceil(B/L) rows per lane (rows past B are zero padding).
 template <int B>
 struct Geo {
-    static constexpr int L = (B == 16) ? 8 : (B == 8) ? 2 : 1;  // lanes per block (== oracle jac_chunks)
-    static constexpr int R = B / L;                              // rows per lane
-    static constexpr int BPW = 64 / L;                           // blocks per wave
-    static constexpr int NW = B * 3 / 4;                         // u32 words per pixel row of a block
-    static constexpr int STRIP_PX = BPW * B;                     // strip width in pixels
+    static constexpr int L = B == 4 ? 1 : B <= 8 ? 2 : B <= 12 ? 4 : 8;
+    static constexpr int R = kRows<B, L>;          // rows per lane
+    static constexpr int BPW = 64 / L;             // blocks per wave
+    static constexpr int NBYTES = B * 3;           // bytes per pixel row of a block
+    static constexpr int NW = (NBYTES + 3) / 4;    // u32 words holding them
+    static constexpr bool WORDS = NBYTES % 4 == 0; // dword I/O possible (b = 4, 8, 12, 16)
 };
+static_assert(Geo<6>::L == 2 && Geo<10>::L == 4 && Geo<14>::L == 8 && Geo<14>::R == 2, "lane layout");
 
-// ---- byte rows -------------------------------------------------------------
-template <int NW>
-TMF_DEVI void load_words(const uint8_t *p, bool aligned, uint32_t (&w)[NW])
+// ---- byte rows: dword I/O when the row segment is whole dwords and aligned,
+// otherwise bytes (b = 6, 10, 14: 18, 30, 42 bytes per row)
+template <int B>
+TMF_DEVI void load_words(const uint8_t *p, bool aligned, uint32_t (&w)[Geo<B>::NW])
 {
-    if (aligned) {
+    constexpr int NW = Geo<B>::NW, NB = Geo<B>::NBYTES;
+    if (Geo<B>::WORDS && aligned) {
         const uint32_t *q = reinterpret_cast<const uint32_t *>(p);
 #pragma unroll
         for (int i = 0; i < NW; ++i) w[i] = q[i];
     } else {
 #pragma unroll
-        for (int i = 0; i < NW; ++i)
-            w[i] = (uint32_t)p[4 * i] | ((uint32_t)p[4 * i + 1] << 8) | ((uint32_t)p[4 * i + 2] << 16) | ((uint32_t)p[4 * i + 3] << 24);
+        for (int i = 0; i < NW; ++i) {
+            uint32_t v = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (4 * i + k < NB) v |= (uint32_t)p[4 * i + k] << (8 * k);
+            w[i] = v;
+        }
     }
 }
 
-template <int NW>
-TMF_DEVI void store_words(uint8_t *p, bool aligned, const uint32_t (&w)[NW])
+template <int B>
+TMF_DEVI void store_words(uint8_t *p, bool aligned, const uint32_t (&w)[Geo<B>::NW])
 {
-    if (aligned) {
+    constexpr int NW = Geo<B>::NW, NB = Geo<B>::NBYTES;
+    if (Geo<B>::WORDS && aligned) {
         uint32_t *q = reinterpret_cast<uint32_t *>(p);
 #pragma unroll
         for (int i = 0; i < NW; ++i) q[i] = w[i];
     } else {
 #pragma unroll
-        for (int i = 0; i < NW; ++i) {
-            p[4 * i] = (uint8_t)w[i];
-            p[4 * i + 1] = (uint8_t)(w[i] >> 8);
-            p[4 * i + 2] = (uint8_t)(w[i] >> 16);
-            p[4 * i + 3] = (uint8_t)(w[i] >> 24);
-        }
+        for (int i = 0; i < NW; ++i)
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (4 * i + k < NB) p[4 * i + k] = (uint8_t)(w[i] >> (8 * k));
     }
 }
 
@@ -83,18 +93,23 @@ TMF_DEVI uint32_t byte_at(const uint32_t *w, int k) { return (w[k >> 2] >> (8 * 
 // ---- LDS-mediated 2-D transforms on a block held in rows layout ---------------
 // tile: this block's [B][B+1] LDS region.  x: this lane's R rows.  Column pass
 // first (axis 0), then rows (watermarking.py:76-83).
+template <int B>
+TMF_DEVI bool real_row(int q, int r) { return Geo<B>::R * Geo<B>::L == B || q * Geo<B>::R + r < B; }
+
 template <int B, bool INVERSE>
 TMF_DEVI void dct2d_rows_layout(float (&x)[Geo<B>::R][B], float *tile, int q)
 {
     constexpr int R = Geo<B>::R, LD = B + 1;
 #pragma unroll
     for (int r = 0; r < R; ++r)
+        if (real_row<B>(q, r))
 #pragma unroll
-        for (int c = 0; c < B; ++c) tile[(q * R + r) * LD + c] = x[r][c];
+            for (int c = 0; c < B; ++c) tile[(q * R + r) * LD + c] = x[r][c];
     __syncthreads();
-    // column pass: this lane takes columns [q*R, q*R+R)
+    // column pass: this lane takes columns [q*R, q*R+R) that exist
 #pragma unroll
     for (int cc = 0; cc < R; ++cc) {
+        if (!real_row<B>(q, cc)) continue;
         float col[B];
 #pragma unroll
         for (int r = 0; r < B; ++r) col[r] = tile[r * LD + q * R + cc];
@@ -107,10 +122,10 @@ TMF_DEVI void dct2d_rows_layout(float (&x)[Geo<B>::R][B], float *tile, int q)
     for (int r = 0; r < R; ++r) {
         float row[B];
 #pragma unroll
-        for (int c = 0; c < B; ++c) row[c] = tile[(q * R + r) * LD + c];
+        for (int c = 0; c < B; ++c) row[c] = real_row<B>(q, r) ? tile[(q * R + r) * LD + c] : 0.0f;
         if constexpr (INVERSE) dct::dct3<B>(row); else dct::dct2<B>(row);
 #pragma unroll
-        for (int c = 0; c < B; ++c) x[r][c] = row[c];
+        for (int c = 0; c < B; ++c) x[r][c] = real_row<B>(q, r) ? row[c] : 0.0f;
     }
     __syncthreads();
 }
@@ -143,9 +158,9 @@ TMF_DEVI void load_block_rows(const uint8_t *frame_base, int W, const StripPos &
     constexpr int R = Geo<B>::R;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        if (pos.valid) {
+        if (pos.valid && real_row<B>(q, r)) {
             const uint8_t *p = frame_base + ((int64_t)(pos.bi * B + q * R + r) * W + (int64_t)pos.bj * B) * 3;
-            load_words<Geo<B>::NW>(p, aligned, words[r]);
+            load_words<B>(p, aligned, words[r]);
         } else {
 #pragma unroll
             for (int i = 0; i < Geo<B>::NW; ++i) words[r][i] = 0u;
@@ -245,8 +260,9 @@ __global__ __launch_bounds__(64) void embed_kernel(EmbedArgs a)
     // N8 (:201): Bm[k][j] = S'[k] * Vt[k][j] (this lane's rows j of V), then M = U @ Bm
 #pragma unroll
     for (int r = 0; r < R; ++r)
+        if (real_row<B>(q, r))
 #pragma unroll
-        for (int k = 0; k < B; ++k) tile[k * LD + q * R + r] = S[k] * Vf[r][k];
+            for (int k = 0; k < B; ++k) tile[k * LD + q * R + r] = S[k] * Vf[r][k];
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -289,7 +305,7 @@ __global__ __launch_bounds__(64) void embed_kernel(EmbedArgs a)
                 out[(k0 + 2) >> 2] |= B8 << (8 * ((k0 + 2) & 3));
             }
             uint8_t *p = dst + ((int64_t)(pos.bi * B + q * R + r) * a.W + (int64_t)pos.bj * B) * 3;
-            store_words<Geo<B>::NW>(p, a.aligned, out);
+            if (real_row<B>(q, r)) store_words<B>(p, a.aligned, out);
         }
     }
     stamp(6);
@@ -422,13 +438,14 @@ __global__ __launch_bounds__(64) void dct2d_blocks_kernel(float *blocks, int64_t
 #pragma unroll
     for (int r = 0; r < R; ++r)
 #pragma unroll
-        for (int c = 0; c < B; ++c) x[r][c] = valid ? blocks[blk * B * B + (q * R + r) * B + c] : 0.0f;
+        for (int c = 0; c < B; ++c) x[r][c] = valid && real_row<B>(q, r) ? blocks[blk * B * B + (q * R + r) * B + c] : 0.0f;
     dct2d_rows_layout<B, INVERSE>(x, lds + g * B * LD, q);
     if (valid)
 #pragma unroll
         for (int r = 0; r < R; ++r)
+            if (real_row<B>(q, r))
 #pragma unroll
-            for (int c = 0; c < B; ++c) blocks[blk * B * B + (q * R + r) * B + c] = x[r][c];
+                for (int c = 0; c < B; ++c) blocks[blk * B * B + (q * R + r) * B + c] = x[r][c];
 }
 
 template <int B>
@@ -443,7 +460,7 @@ __global__ __launch_bounds__(64) void svd_blocks_kernel(const float *__restrict_
 #pragma unroll
     for (int r = 0; r < R; ++r)
 #pragma unroll
-        for (int c = 0; c < B; ++c) x[r][c] = valid ? D[blk * B * B + (q * R + r) * B + c] : 0.0f;
+        for (int c = 0; c < B; ++c) x[r][c] = valid && real_row<B>(q, r) ? D[blk * B * B + (q * R + r) * B + c] : 0.0f;
     double A[R][B], V[R][B];
     int nsw = svd3<B, L>(x, A, V, q);
     double sig[B];
@@ -488,11 +505,12 @@ __global__ __launch_bounds__(64) void svd_blocks_kernel(const float *__restrict_
     if (!valid) return;
 #pragma unroll
     for (int r = 0; r < R; ++r)
+        if (real_row<B>(q, r))
 #pragma unroll
-        for (int k = 0; k < B; ++k) {
-            U[blk * B * B + (q * R + r) * B + k] = Uf[r][k];
-            Vt[blk * B * B + k * B + q * R + r] = Vf[r][k];
-        }
+            for (int k = 0; k < B; ++k) {
+                U[blk * B * B + (q * R + r) * B + k] = Uf[r][k];
+                Vt[blk * B * B + k * B + q * R + r] = Vf[r][k];
+            }
     if (q == 0) {
 #pragma unroll
         for (int k = 0; k < B; ++k) S[blk * B + k] = (float)sig[k];
@@ -553,7 +571,11 @@ hipError_t launch_embed(const EmbedArgs &a, hipStream_t st)
     if (a.nbh > 0 && a.nbw > 0) {
         switch (a.block) {
         case 4: e = launch_embed_b<4>(a, st); break;
+        case 6: e = launch_embed_b<6>(a, st); break;
         case 8: e = launch_embed_b<8>(a, st); break;
+        case 10: e = launch_embed_b<10>(a, st); break;
+        case 12: e = launch_embed_b<12>(a, st); break;
+        case 14: e = launch_embed_b<14>(a, st); break;
         case 16: e = launch_embed_b<16>(a, st); break;
         default: return hipErrorInvalidValue;
         }
@@ -606,7 +628,11 @@ hipError_t launch_extract(const ExtractArgs &a, hipStream_t st)
     if (a.nbh == 0 || a.nbw == 0) return hipSuccess;
     switch (a.block) {
     case 4: return launch_extract_b<4>(a, st);
+    case 6: return launch_extract_b<6>(a, st);
     case 8: return launch_extract_b<8>(a, st);
+    case 10: return launch_extract_b<10>(a, st);
+    case 12: return launch_extract_b<12>(a, st);
+    case 14: return launch_extract_b<14>(a, st);
     case 16: return launch_extract_b<16>(a, st);
     default: return hipErrorInvalidValue;
     }
@@ -640,7 +666,11 @@ hipError_t launch_dct2d_blocks(float *blocks, int64_t nb, int block, int inverse
     if (nb == 0) return hipSuccess;
     switch (block) {
     case 4: return launch_dct_b<4>(blocks, nb, inverse, st);
+    case 6: return launch_dct_b<6>(blocks, nb, inverse, st);
     case 8: return launch_dct_b<8>(blocks, nb, inverse, st);
+    case 10: return launch_dct_b<10>(blocks, nb, inverse, st);
+    case 12: return launch_dct_b<12>(blocks, nb, inverse, st);
+    case 14: return launch_dct_b<14>(blocks, nb, inverse, st);
     case 16: return launch_dct_b<16>(blocks, nb, inverse, st);
     default: return hipErrorInvalidValue;
     }
@@ -659,7 +689,11 @@ hipError_t launch_svd_blocks(const float *D, int64_t nb, int block, float *U, fl
     if (nb == 0) return hipSuccess;
     switch (block) {
     case 4: return launch_svd_b<4>(D, nb, U, S, Vt, sweeps, st);
+    case 6: return launch_svd_b<6>(D, nb, U, S, Vt, sweeps, st);
     case 8: return launch_svd_b<8>(D, nb, U, S, Vt, sweeps, st);
+    case 10: return launch_svd_b<10>(D, nb, U, S, Vt, sweeps, st);
+    case 12: return launch_svd_b<12>(D, nb, U, S, Vt, sweeps, st);
+    case 14: return launch_svd_b<14>(D, nb, U, S, Vt, sweeps, st);
     case 16: return launch_svd_b<16>(D, nb, U, S, Vt, sweeps, st);
     default: return hipErrorInvalidValue;
     }

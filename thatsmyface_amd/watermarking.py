@@ -10,8 +10,8 @@ per-pixel and per-block loop runs in libtmfwm.so's HIP kernels and returns
 the reference's bytes.  There is no CPU fallback: without the
 built library or a GPU these functions raise.
 
-Deviations: block sizes other than 4, 8, 16 raise
-NotImplementedError; an original image smaller than the watermarked one raises
+Deviations: block sizes other than the app's slider values
+(4..16 step 2) raise NotImplementedError; an original image smaller than the watermarked one raises
 ValueError (the reference raises for a full block of shortfall and silently
 computes partial blocks for less); array inputs to the helper functions must be
 uint8 RGB(A) / float32 as the reference itself produces them.
