@@ -43,7 +43,7 @@ extern "C" {
 #define TMFWM_ERR_INVALID (-22)     /* bad argument (EINVAL) */
 #define TMFWM_ERR_NOMEM (-12)       /* device allocation failed (ENOMEM) */
 #define TMFWM_ERR_HIP (-5)          /* HIP runtime / launch error (EIO) */
-#define TMFWM_ERR_UNSUPPORTED (-95) /* block size not 4/8/16 (EOPNOTSUPP) */
+#define TMFWM_ERR_UNSUPPORTED (-95) /* block size not an even 4..16 (EOPNOTSUPP) */
 #define TMFWM_ERR_NODEVICE (-19)    /* no usable gfx950 device (ENODEV) */
 
 /* ABI version (TMFWM_ABI_VERSION) compiled into the library. */
@@ -98,6 +98,20 @@ int tmfwm_svd_blocks(const float *D, int64_t n_blocks, int32_t block, float *U, 
  * out[f*frame_bytes + i] = splitmix64(seed ^ ((frame0+f) << 40) ^ i) & 0xFF. */
 int tmfwm_synth_frames(uint64_t seed, int64_t frame0, int64_t n_frames, int64_t frame_bytes, uint8_t *out,
                        void *hip_stream);
+
+/*
+ * Watermark preparation: replaces resize_watermark() (watermarking.py:86-132)
+ * after its PNG decode and convert("L") (:98-103), which stay with the caller.
+ * wm: wm_height x wm_width 8-bit grey pixels.  tile: tile_height x tile_width.
+ * preserve_ratio = 0: Pillow 12.2.0 Image.resize((tile_width, tile_height),
+ * LANCZOS) (:127-130).  preserve_ratio != 0: LANCZOS to (int(w*r), int(h*r)),
+ * r = min(tile_width/w, tile_height/h), pasted centred on a white (255) canvas
+ * (:105-123).  Bytes equal Pillow's (fixed-point Resample.c).  Synchronises
+ * `hip_stream` before returning (the resample tables are built on the host).
+ * Empty sizes return TMFWM_ERR_INVALID (PIL raises ValueError there).
+ */
+int tmfwm_prepare_tile(const uint8_t *wm, int32_t wm_height, int32_t wm_width, int32_t tile_height, int32_t tile_width,
+                       int32_t preserve_ratio, uint8_t *tile, int32_t mem_kind, void *hip_stream);
 
 #ifdef __cplusplus
 }

@@ -54,6 +54,8 @@ def lib():
             "orc_embed_batch": (I32, [_u8p, I64, I32, I32, _u8p, I32, D, _u8p, I32]),
             "orc_extract_batch": (I32, [_u8p, _u8p, I64, I32, I32, I32, D, _u8p, I32]),
             "orc_synth_bytes": (None, [ctypes.c_uint64, I64, I64, I64, _u8p]),
+            "orc_resize_lanczos": (I32, [_u8p, I32, I32, I32, I32, _u8p, I32]),
+            "orc_prepare_tile": (I32, [_u8p, I32, I32, I32, I32, I32, _u8p]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -194,4 +196,21 @@ def extract_batch(wrgb: np.ndarray, orgb: np.ndarray, block: int, alpha: float, 
 def synth_bytes(seed: int, frame0: int, nframes: int, frame_bytes: int) -> np.ndarray:
     out = np.empty(nframes * frame_bytes, np.uint8)
     lib().orc_synth_bytes(ctypes.c_uint64(seed), frame0, nframes, frame_bytes, _p(out, _u8p))
+    return out
+
+
+# --- watermark preparation (watermarking.py:102-132 after convert("L")) ------
+def resize_lanczos(img: np.ndarray, oh: int, ow: int) -> np.ndarray:
+    img = np.ascontiguousarray(img, np.uint8)
+    out = np.empty((oh, ow), np.uint8)
+    if lib().orc_resize_lanczos(_p(img, _u8p), img.shape[0], img.shape[1], oh, ow, _p(out, _u8p), ow):
+        raise ValueError("empty size")
+    return out
+
+
+def prepare_tile(wm_l: np.ndarray, th: int, tw: int, preserve_ratio: bool) -> np.ndarray:
+    wm_l = np.ascontiguousarray(wm_l, np.uint8)
+    out = np.empty((th, tw), np.uint8)
+    if lib().orc_prepare_tile(_p(wm_l, _u8p), wm_l.shape[0], wm_l.shape[1], th, tw, int(bool(preserve_ratio)), _p(out, _u8p)):
+        raise ValueError("empty size")
     return out

@@ -1109,6 +1109,142 @@ int orc_extract_batch(const uint8_t *wrgb, const uint8_t *orgb, int64_t n, int H
     return 0;
 }
 
+/* ------------------------------------------------------------------------ */
+/* Watermark preparation (watermarking.py:102-132 after convert("L")):      */
+/* Pillow 12.2.0 Image.resize(LANCZOS) on an 8-bit L image -- Resample.c    */
+/* precompute_coeffs (double), normalize_coeffs_8bpc (22-bit fixed point),  */
+/* horizontal pass over the used rows, then vertical pass -- and the        */
+/* ratio-preserving paste on a white canvas.  Pillow is the reference's     */
+/* third-party dependency; parity is pinned against PIL itself and the      */
+/* golden tiles (tests/test_oracle_golden.py).                              */
+/* ------------------------------------------------------------------------ */
+#define RS_PRECISION_BITS (32 - 8 - 2)
+
+static double rs_sinc(double x)
+{
+    if (x == 0.0) return 1.0;
+    x = x * 3.14159265358979323846; /* M_PI */
+    return sin(x) / x;
+}
+
+static double rs_lanczos(double x) { return (-3.0 <= x && x < 3.0) ? rs_sinc(x) * rs_sinc(x / 3) : 0.0; }
+
+/* returns ksize; bounds[2*out], kk[out*ksize] (fixed point) are malloc'ed */
+static int rs_coeffs(int inSize, int outSize, int **boundsp, int32_t **kkp)
+{
+    const float in0 = 0.0f, in1 = (float)inSize; /* box = (0, 0, w, h) as floats */
+    double filterscale, scale;
+    filterscale = scale = (double)(in1 - in0) / outSize;
+    if (filterscale < 1.0) filterscale = 1.0;
+    const double support = 3.0 * filterscale;
+    const int ksize = (int)ceil(support) * 2 + 1;
+    double *kd = (double *)malloc(sizeof(double) * (size_t)outSize * ksize);
+    int *bounds = (int *)malloc(sizeof(int) * (size_t)outSize * 2);
+    int32_t *kk = (int32_t *)malloc(sizeof(int32_t) * (size_t)outSize * ksize);
+    for (int xx = 0; xx < outSize; xx++) {
+        const double center = in0 + (xx + 0.5) * scale, ss = 1.0 / filterscale;
+        double ww = 0.0;
+        int xmin = (int)(center - support + 0.5);
+        if (xmin < 0) xmin = 0;
+        int xmax = (int)(center + support + 0.5);
+        if (xmax > inSize) xmax = inSize;
+        xmax -= xmin;
+        double *k = kd + (size_t)xx * ksize;
+        int x;
+        for (x = 0; x < xmax; x++) {
+            const double w = rs_lanczos((x + xmin - center + 0.5) * ss);
+            k[x] = w;
+            ww += w;
+        }
+        for (x = 0; x < xmax; x++)
+            if (ww != 0.0) k[x] /= ww;
+        for (; x < ksize; x++) k[x] = 0;
+        bounds[xx * 2] = xmin;
+        bounds[xx * 2 + 1] = xmax;
+    }
+    for (size_t i = 0; i < (size_t)outSize * ksize; i++)
+        kk[i] = kd[i] < 0 ? (int)(-0.5 + kd[i] * (1 << RS_PRECISION_BITS)) : (int)(0.5 + kd[i] * (1 << RS_PRECISION_BITS));
+    free(kd);
+    *boundsp = bounds;
+    *kkp = kk;
+    return ksize;
+}
+
+static uint8_t rs_clip8(int v)
+{
+    v >>= RS_PRECISION_BITS;
+    return v < 0 ? 0 : v > 255 ? 255 : (uint8_t)v;
+}
+
+/* Image.resize((ow, oh), Image.LANCZOS) of an ih x iw L image into out (oh x ow,
+ * row stride ldo).  Returns -1 for an empty size (PIL raises). */
+int orc_resize_lanczos(const uint8_t *in, int ih, int iw, int oh, int ow, uint8_t *out, int ldo)
+{
+    if (ih <= 0 || iw <= 0 || oh <= 0 || ow <= 0) return -1;
+    if (oh == ih && ow == iw) { /* Image.resize returns a copy */
+        for (int y = 0; y < oh; y++) memcpy(out + (size_t)y * ldo, in + (size_t)y * iw, (size_t)iw);
+        return 0;
+    }
+    int *bh, *bv;
+    int32_t *kh, *kv;
+    const int need_h = ow != iw, need_v = oh != ih;
+    const int ksh = rs_coeffs(iw, ow, &bh, &kh), ksv = rs_coeffs(ih, oh, &bv, &kv);
+    const int yfirst = bv[0], ylast = bv[oh * 2 - 2] + bv[oh * 2 - 1];
+    const uint8_t *src = in;
+    int sw = iw;
+    uint8_t *tmp = NULL;
+    if (need_h) {
+        for (int i = 0; i < oh; i++) bv[i * 2] -= yfirst;
+        const int sh = ylast - yfirst;
+        tmp = (uint8_t *)malloc((size_t)sh * ow + 1);
+        for (int yy = 0; yy < sh; yy++)
+            for (int xx = 0; xx < ow; xx++) {
+                const int xmin = bh[xx * 2], xmax = bh[xx * 2 + 1];
+                const int32_t *k = kh + (size_t)xx * ksh;
+                int ss0 = 1 << (RS_PRECISION_BITS - 1);
+                for (int x = 0; x < xmax; x++) ss0 += (int)in[(size_t)(yy + yfirst) * iw + x + xmin] * k[x];
+                tmp[(size_t)yy * ow + xx] = rs_clip8(ss0);
+            }
+        src = tmp;
+        sw = ow;
+    }
+    if (need_v) {
+        for (int yy = 0; yy < oh; yy++) {
+            const int32_t *k = kv + (size_t)yy * ksv;
+            const int ymin = bv[yy * 2], ymax = bv[yy * 2 + 1];
+            for (int xx = 0; xx < sw; xx++) {
+                int ss0 = 1 << (RS_PRECISION_BITS - 1);
+                for (int y = 0; y < ymax; y++) ss0 += (int)src[(size_t)(y + ymin) * sw + xx] * k[y];
+                out[(size_t)yy * ldo + xx] = rs_clip8(ss0);
+            }
+        }
+    } else {
+        for (int y = 0; y < oh; y++) memcpy(out + (size_t)y * ldo, src + (size_t)y * sw, (size_t)sw);
+    }
+    free(tmp);
+    free(bh);
+    free(bv);
+    free(kh);
+    free(kv);
+    return 0;
+}
+
+/* resize_watermark (watermarking.py:105-132) on an already-"L" watermark:
+ * preserve_ratio -> LANCZOS to (int(w*ratio), int(h*ratio)), centred on a white
+ * th x tw canvas; otherwise LANCZOS straight to th x tw. */
+int orc_prepare_tile(const uint8_t *wm, int wh, int ww, int th, int tw, int preserve_ratio, uint8_t *tile)
+{
+    if (wh <= 0 || ww <= 0 || th <= 0 || tw <= 0) return -1;
+    if (!preserve_ratio) return orc_resize_lanczos(wm, wh, ww, th, tw, tile, tw);
+    const double rw = (double)tw / (double)ww, rh = (double)th / (double)wh;
+    const double ratio = rw < rh ? rw : rh; /* Python min() keeps the first of equals */
+    const int nw = (int)((double)ww * ratio), nh = (int)((double)wh * ratio);
+    if (nw <= 0 || nh <= 0) return -1;
+    memset(tile, 255, (size_t)th * tw);
+    const int px = (tw - nw) / 2, py = (th - nh) / 2;
+    return orc_resize_lanczos(wm, wh, ww, nh, nw, tile + (size_t)py * tw + px, tw);
+}
+
 /* Synthetic input generator shared with the GPU generator:
  * byte = splitmix64(seed ^ (frame << 40) ^ idx) & 0xFF over the linear HWC index. */
 static inline uint64_t splitmix64(uint64_t x)

@@ -30,23 +30,6 @@ def test_settings_from_session_state(monkeypatch):
     assert W.get_watermark_settings() == {"block_size": 8, "alpha": 0.1}
 
 
-def test_resize_watermark_matches_reference_tiles(golden):
-    cases, meta = golden
-    for name, m in meta["cases"].items():
-        wm = cases[f"{name}/wm"]
-        b = m["block"]
-        cov = cases[f"{name}/cover"]
-        nbh, nbw = cov.shape[0] // b, cov.shape[1] // b
-        src = Image.fromarray(wm, "L")
-        if m["wm_as_png_bytes"]:
-            buf = io.BytesIO()
-            src.save(buf, format="PNG")
-            src = buf.getvalue()
-        tile = W.resize_watermark(src, nbh, nbw, m["preserve_ratio"])
-        assert tile.mode == "L"
-        assert np.array_equal(np.asarray(tile), cases[f"{name}/tile"]), name
-
-
 def test_extract_rejects_smaller_original():
     big = Image.new("RGB", (64, 64))
     with pytest.raises(ValueError, match="smaller"):

@@ -43,6 +43,7 @@ SIGNATURES = {
     "tmfwm_dct2d_blocks": (ctypes.c_int, [_VP, _I64, _I32, _I32, _I32, _VP]),
     "tmfwm_svd_blocks": (ctypes.c_int, [_VP, _I64, _I32, _VP, _VP, _VP, _VP, _I32, _VP]),
     "tmfwm_synth_frames": (ctypes.c_int, [ctypes.c_uint64, _I64, _I64, _I64, _VP, _VP]),
+    "tmfwm_prepare_tile": (ctypes.c_int, [_VP, _I32, _I32, _I32, _I32, _I32, _VP, _I32, _VP]),
 }
 
 _lock = threading.Lock()

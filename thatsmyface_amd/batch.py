@@ -109,3 +109,23 @@ def svd_blocks(D: torch.Tensor):
         _lib.check(L.tmfwm_svd_blocks(D.data_ptr(), n, b, U.data_ptr(), S.data_ptr(), Vt.data_ptr(), sw.data_ptr(),
                                       _lib.MEM_DEVICE, _stream(None)), "svd_blocks")
     return U, S, Vt, sw
+
+
+def prepare_tile(watermark_l: torch.Tensor, tile_height: int, tile_width: int, preserve_ratio: bool = False,
+                 out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+    """resize_watermark (watermarking.py:105-130) on a device-resident (h, w) uint8 grey
+    watermark: Pillow-exact LANCZOS resample (+ centred paste on white when
+    preserve_ratio).  Synchronises the stream (the resample tables come from the host)."""
+    if not watermark_l.is_cuda or watermark_l.dtype != torch.uint8 or watermark_l.dim() != 2:
+        raise ValueError("watermark_l must be a (h, w) uint8 GPU tensor")
+    watermark_l = watermark_l.contiguous()
+    if out is None:
+        out = torch.empty((tile_height, tile_width), dtype=torch.uint8, device=watermark_l.device)
+    elif tuple(out.shape) != (tile_height, tile_width) or out.dtype != torch.uint8 or not out.is_contiguous():
+        raise ValueError("out must be a contiguous (tile_height, tile_width) uint8 tensor")
+    with torch.cuda.device(watermark_l.device):
+        L = _lib.load()
+        _lib.check(L.tmfwm_prepare_tile(watermark_l.data_ptr(), watermark_l.shape[0], watermark_l.shape[1], tile_height,
+                                        tile_width, int(bool(preserve_ratio)), out.data_ptr(), _lib.MEM_DEVICE, _stream(stream)),
+                   "prepare_tile")
+    return out

@@ -7,6 +7,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <string>
+#include <vector>
 
 #include "../../include/tmfwm.h"
 #include "tmfwm_internal.h"
@@ -341,6 +342,59 @@ int tmfwm_synth_frames(uint64_t seed, int64_t frame0, int64_t n_frames, int64_t 
     if (int rc = need_device()) return rc;
     if (int rc = check_device_ptr(out, "out")) return rc;
     TMF_HIP(tmf::launch_synth(seed, frame0, n_frames, frame_bytes, out, pick_stream(hip_stream)));
+    return 0;
+}
+
+int tmfwm_prepare_tile(const uint8_t *wm, int32_t wm_height, int32_t wm_width, int32_t tile_height, int32_t tile_width,
+                       int32_t preserve_ratio, uint8_t *tile, int32_t mem_kind, void *hip_stream)
+{
+    t_err.clear();
+    if (wm_height <= 0 || wm_width <= 0 || tile_height <= 0 || tile_width <= 0)
+        return fail(TMFWM_ERR_INVALID, "height and width must be > 0 (watermark %dx%d, tile %dx%d)", wm_width, wm_height,
+                    tile_width, tile_height);
+    if (mem_kind != TMFWM_MEM_HOST && mem_kind != TMFWM_MEM_DEVICE) return fail(TMFWM_ERR_INVALID, "mem_kind %d", mem_kind);
+    // watermarking.py:105-110: ratio = min(tw/ow, th/oh); new size int(size * ratio)
+    int rh = tile_height, rw = tile_width, px = 0, py = 0;
+    if (preserve_ratio) {
+        const double fw = (double)tile_width / (double)wm_width, fh = (double)tile_height / (double)wm_height;
+        const double ratio = fh < fw ? fh : fw;  // Python min() keeps the first of equals
+        rw = (int)((double)wm_width * ratio);
+        rh = (int)((double)wm_height * ratio);
+        if (rw <= 0 || rh <= 0) return fail(TMFWM_ERR_INVALID, "height and width must be > 0 (resized %dx%d)", rw, rh);
+        px = (tile_width - rw) / 2;  // :120-121
+        py = (tile_height - rh) / 2;
+    }
+    if (mem_kind == TMFWM_MEM_DEVICE) {
+        if (int rc = check_device_ptr(wm, "wm")) return rc;
+        if (int rc = check_device_ptr(tile, "tile")) return rc;
+    } else if (!wm || !tile) {
+        return fail(TMFWM_ERR_INVALID, "NULL host pointer");
+    }
+    if (int rc = need_device()) return rc;
+    hipStream_t st = pick_stream(hip_stream);
+    tmf::ResamplePlan plan;
+    plan.build(wm_height, wm_width, rh, rw);
+    const std::vector<int> tables = plan.pack();
+    const size_t wbytes = (size_t)wm_height * wm_width, tbytes = (size_t)tile_height * tile_width;
+    DevBuf dtab, dtmp, dwm, dtile;
+    if (int rc = dtab.alloc(tables.size() * sizeof(int), st, "resample tables")) return rc;
+    if (int rc = dtmp.alloc(plan.tmp_bytes(), st, "resample scratch")) return rc;
+    const uint8_t *src = wm;
+    uint8_t *dst = tile;
+    if (mem_kind == TMFWM_MEM_HOST) {
+        if (int rc = dwm.alloc(wbytes, st, "watermark")) return rc;
+        if (int rc = dtile.alloc(tbytes, st, "tile")) return rc;
+        TMF_HIP(hipMemcpyAsync(dwm.p, wm, wbytes, hipMemcpyHostToDevice, st));
+        src = static_cast<const uint8_t *>(dwm.p);
+        dst = static_cast<uint8_t *>(dtile.p);
+    }
+    TMF_HIP(hipMemcpyAsync(dtab.p, tables.data(), tables.size() * sizeof(int), hipMemcpyHostToDevice, st));
+    if (preserve_ratio) TMF_HIP(hipMemsetAsync(dst, 255, tbytes, st));  // Image.new("L", ..., 255) (:116)
+    TMF_HIP(tmf::launch_resize_lanczos(src, plan, static_cast<const int *>(dtab.p), static_cast<uint8_t *>(dtmp.p),
+                                       dst + (size_t)py * tile_width + px, tile_width, st));
+    if (mem_kind == TMFWM_MEM_HOST) TMF_HIP(hipMemcpyAsync(tile, dst, tbytes, hipMemcpyDeviceToHost, st));
+    // the host-side tables (and, for the host path, the result) must outlive the copies
+    TMF_HIP(hipStreamSynchronize(st));
     return 0;
 }
 

@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <vector>
+
 namespace tmf {
 
 struct EmbedArgs {
@@ -42,6 +44,26 @@ hipError_t launch_rgb_to_ycbcr(const uint8_t *rgb, int64_t npix, float *ycc, hip
 hipError_t launch_ycbcr_to_rgb(const float *ycc, int64_t npix, uint8_t *rgb, hipStream_t st);
 hipError_t launch_dct2d_blocks(float *blocks, int64_t nb, int block, int inverse, hipStream_t st);
 hipError_t launch_svd_blocks(const float *D, int64_t nb, int block, float *U, float *S, float *Vt, int32_t *sweeps, hipStream_t st);
+// Watermark-tile preparation (tmfwm_tile.hip): Pillow's LANCZOS resample tables.
+struct ResampleAxis {
+    int ksize = 0;
+    std::vector<int> bounds;  // 2 per output sample: first input index, count
+    std::vector<int> kk;      // ksize 22-bit fixed-point taps per output sample
+    void build(int in_size, int out_size);
+};
+
+struct ResamplePlan {
+    int ih = 0, iw = 0, oh = 0, ow = 0, y_first = 0, y_last = 0;
+    bool need_h = false, need_v = false;
+    ResampleAxis h, v;
+    void build(int in_h, int in_w, int out_h, int out_w);
+    int rows() const { return y_last - y_first; }
+    size_t tmp_bytes() const { return need_h ? (size_t)rows() * ow : 0; }
+    std::vector<int> pack() const;  // [bounds_h | kk_h | bounds_v | kk_v]
+};
+
+hipError_t launch_resize_lanczos(const uint8_t *in, const ResamplePlan &plan, const int *tables, uint8_t *tmp, uint8_t *out,
+                                 int ldo, hipStream_t st);
 hipError_t launch_synth(uint64_t seed, int64_t frame0, int64_t nframes, int64_t frame_bytes, uint8_t *out, hipStream_t st);
 
 }  // namespace tmf

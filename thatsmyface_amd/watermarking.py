@@ -4,10 +4,10 @@ Same module surface and signatures as the reference
 (/root/reference/modules/watermarking.py): ``get_watermark_settings`` (:10),
 ``rgb_to_ycbcr`` (:23), ``ycbcr_to_rgb`` (:53), ``apply_dct_to_block`` (:76),
 ``apply_idct_to_block`` (:81), ``resize_watermark`` (:86), ``embed_watermark``
-(:135), ``extract_watermark`` (:224).  The host keeps the reference's PIL
-preparation (mode conversion, watermark decode + LANCZOS resize); every
-per-pixel and per-block loop runs in libtmfwm.so's HIP kernels and returns
-the reference's bytes.  There is no CPU fallback: without the
+(:135), ``extract_watermark`` (:224).  The host keeps PIL for image decode and
+mode conversion only; the watermark's LANCZOS resample and every per-pixel and
+per-block loop run in libtmfwm.so's HIP kernels and return the reference's
+bytes.  There is no CPU fallback: without the
 built library or a GPU these functions raise.
 
 Deviations: block sizes other than the app's slider values
@@ -121,19 +121,19 @@ def apply_idct_to_block(block) -> np.ndarray:
 
 
 def resize_watermark(watermark, target_height, target_width, preserve_ratio=False):
-    """watermarking.py:86-132, same PIL operations (host side by design)."""
+    """watermarking.py:86-132.  PNG decode and convert("L") (:98-103) stay with PIL on
+    the host; the LANCZOS resample and the white-canvas paste (:105-130) run on the GPU
+    (tmfwm_prepare_tile), byte-identical to Pillow's fixed-point resampler."""
     watermark_img = Image.open(io.BytesIO(watermark)) if isinstance(watermark, bytes) else watermark
-    watermark_img = watermark_img.convert("L")
-    if preserve_ratio:
-        original_width, original_height = watermark_img.size
-        ratio = min(target_width / original_width, target_height / original_height)
-        new_width = int(original_width * ratio)
-        new_height = int(original_height * ratio)
-        resized = watermark_img.resize((new_width, new_height), Image.LANCZOS)
-        final = Image.new("L", (target_width, target_height), 255)
-        final.paste(resized, ((target_width - new_width) // 2, (target_height - new_height) // 2))
-        return final
-    return watermark_img.resize((target_width, target_height), Image.LANCZOS)
+    grey = np.ascontiguousarray(np.asarray(watermark_img.convert("L"), dtype=np.uint8))
+    th, tw = int(target_height), int(target_width)
+    if th <= 0 or tw <= 0 or grey.size == 0:
+        raise ValueError("height and width must be > 0")
+    tile = np.empty((th, tw), np.uint8)
+    L = _lib.load()
+    _lib.check(L.tmfwm_prepare_tile(_ptr(grey), grey.shape[0], grey.shape[1], th, tw, int(bool(preserve_ratio)), _ptr(tile),
+                                    _lib.MEM_HOST, None), "resize_watermark")
+    return Image.fromarray(tile, "L")
 
 
 def _settings(custom_settings):
