@@ -669,6 +669,8 @@ TMF_DEVI double dpp(double v)
 }
 template <int CTRL>
 TMF_DEVI float dpp(float v) { return __builtin_bit_cast(float, dpp_i<CTRL>(__builtin_bit_cast(int, v))); }
+template <int CTRL>
+TMF_DEVI int dpp(int v) { return dpp_i<CTRL>(v); }
 
 template <int PATTERN>
 TMF_DEVI double swz(double v)
@@ -679,6 +681,8 @@ TMF_DEVI double swz(double v)
 }
 template <int PATTERN>
 TMF_DEVI float swz(float v) { return __builtin_bit_cast(float, swz_i<PATTERN>(__builtin_bit_cast(int, v))); }
+template <int PATTERN>
+TMF_DEVI int swz(int v) { return swz_i<PATTERN>(v); }
 
 // Butterfly sum over the L lanes of a group == the oracle's pairwise tree:
 // level 3 pairs lane i with 7-i, whose value (p6+p7)+(p4+p5) equals (p4+p5)+(p6+p7) bitwise.
@@ -807,6 +811,7 @@ TMF_DEVI int jacobi(T (&A)[(B + L - 1) / L][B], T (&V)[(B + L - 1) / L][B], int 
     using P = JacP<T>;
     // NP pairs per round; lane q evaluates pairs [q*PP, q*PP + PP) that exist
     constexpr int R = kRows<B, L>, NP = B / 2, PP = (NP + L - 1) / L;
+    constexpr bool kBranchy = P::kBranchy;
     T F = T(0);
     static_for<B>([&](auto K) { F += cdot<R, B, L>(A, K, K); });
     const T c2 = P::kC2 * F;
@@ -825,21 +830,18 @@ TMF_DEVI int jacobi(T (&A)[(B + L - 1) / L][B], T (&V)[(B + L - 1) / L][B], int 
         static_for<B - 1>([&](auto S) {
             constexpr int s = S;
             T ga[NP];
-            bool on[NP];
             static_for<NP>([&](auto Pi) {
                 constexpr int p = Pi, i = Sched<B>::lo(s, p), j = Sched<B>::hi(s, p);
                 ga[p] = cdot<R, B, L>(A, i, j);
-                const T g2 = ga[p] * ga[p];
-                bool skip = g2 <= c2 * (nrm[i] + nrm[j]) || g2 <= (P::kTol2 * nrm[i]) * nrm[j];
-                if constexpr (std::is_same_v<T, float>) skip = skip || g2 <= c2a || !live;
-                on[p] = !skip;
             });
-            // parameters of this lane's pairs
+            // this lane's pairs: select (alpha, beta, gamma), evaluate the rotation test
+            // (only here -- the owner's flag travels with its parameters), rotation
             Rot<T> mine[PP];
+            int own_on[PP];
             static_for<PP>([&](auto U) {
                 constexpr int p0 = U, i0 = Sched<B>::lo(s, p0), j0 = Sched<B>::hi(s, p0);
                 T a = nrm[i0], b = nrm[j0], g = ga[p0];
-                bool o = on[p0];
+                int slot = -1;  // lane has a U-th pair this round
                 static_for<L - 1>([&](auto Q1) {
                     constexpr int QQ = Q1 + 1, p = QQ * PP + U;
                     int m = -(int)(q == QQ);
@@ -849,13 +851,17 @@ TMF_DEVI int jacobi(T (&A)[(B + L - 1) / L][B], T (&V)[(B + L - 1) / L][B], int 
                         a = blend(m, nrm[i], a);
                         b = blend(m, nrm[j], b);
                         g = blend(m, ga[p], g);
-                        o = (m & (int)on[p]) | (~m & (int)o);
                     } else {
-                        o = ~m & (int)o;  // lane QQ has no U-th pair this round
+                        slot &= ~m;
                     }
                 });
+                const T g2 = g * g;
+                bool skip = g2 <= c2 * (a + b) || g2 <= (P::kTol2 * a) * b;
+                if constexpr (std::is_same_v<T, float>) skip = skip || g2 <= c2a || !live;
+                const bool o = slot != 0 && !skip;
+                own_on[U] = (int)o;
                 mine[U] = Rot<T>{T(1), T(0), T(0)};
-                if (!P::kBranchy || __any(o)) {  // wave-uniform: every lane computes, non-rotating lanes keep identity
+                if (!kBranchy || __any(o)) {  // wave-uniform: every lane computes, non-rotating lanes keep identity
                     const Rot<T> r = rotation(a, b, g);
                     mine[U].c = o ? r.c : T(1);
                     mine[U].s = o ? r.s : T(0);
@@ -867,12 +873,13 @@ TMF_DEVI int jacobi(T (&A)[(B + L - 1) / L][B], T (&V)[(B + L - 1) / L][B], int 
                 const T c = group_bcast<L, src>(mine[u].c);
                 const T sn = group_bcast<L, src>(mine[u].s);
                 const T tg = group_bcast<L, src>(mine[u].tg);
-                rotated |= (int)on[p];
+                const int on = group_bcast<L, src>(own_on[u]);
+                rotated |= on;
                 // Wave-uniform branch; lanes whose block skips this pair apply the identity
                 // (c, s, t*gamma) = (1, 0, 0): fma(-0, y, 1*x) == x bitwise for every value
                 // A (phase 3) and V can hold (their fma chains start from +0 and never make
                 // -0), and A32 / phase-1 A only feed cdot(), which ignores signs of zero.
-                if (!P::kBranchy || __any(on[p])) {
+                if (!kBranchy || __any(on)) {
                     nrm[i] = nrm[i] - tg;
                     nrm[j] = nrm[j] + tg;
 #pragma unroll

@@ -349,19 +349,30 @@ TMF_DEVI float sigma1_of(const uint32_t (&words)[Geo<B>::R][Geo<B>::NW], int q, 
 }
 
 template <int B>
-__global__ __launch_bounds__(64) void extract_kernel(ExtractArgs a)
+__global__ __launch_bounds__(64, (B > 8 ? 2 : 3)) void extract_kernel(ExtractArgs a)  // waves per SIMD
 {
     constexpr int L = Geo<B>::L, BPW = Geo<B>::BPW, LD = B + 1;
     __shared__ float lds[BPW * B * LD];
     const int lane = threadIdx.x & 63, g = lane / L, q = lane % L;
     float *tile = lds + g * B * LD;
     const StripPos pos = strip_pos<B>(a.strips_per_row, a.nbw);
-    // both images' rows are requested up front: one exposed HBM latency per wave, not two
-    uint32_t ww[Geo<B>::R][Geo<B>::NW], wo[Geo<B>::R][Geo<B>::NW];
-    load_block_rows<B>(a.wsrc + pos.frame * a.frame_stride, a.W, pos, q, a.aligned, ww);
-    load_block_rows<B>(a.osrc + pos.frame * a.frame_stride, a.W, pos, q, a.aligned, wo);
-    const float sw = sigma1_of<B>(ww, q, tile);
-    const float so = sigma1_of<B>(wo, q, tile);
+    // b <= 12: both images' rows are requested up front -- one exposed HBM latency per
+    // wave, not two (~4 % at b = 8, and only at 3 waves/SIMD, hence the launch bound).
+    // b >= 14: the extra live rows would push the fallback Jacobi into spills.
+    float sw, so;
+    if constexpr (B <= 12) {
+        uint32_t ww[Geo<B>::R][Geo<B>::NW], wo[Geo<B>::R][Geo<B>::NW];
+        load_block_rows<B>(a.wsrc + pos.frame * a.frame_stride, a.W, pos, q, a.aligned, ww);
+        load_block_rows<B>(a.osrc + pos.frame * a.frame_stride, a.W, pos, q, a.aligned, wo);
+        sw = sigma1_of<B>(ww, q, tile);
+        so = sigma1_of<B>(wo, q, tile);
+    } else {
+        uint32_t w[Geo<B>::R][Geo<B>::NW];
+        load_block_rows<B>(a.wsrc + pos.frame * a.frame_stride, a.W, pos, q, a.aligned, w);
+        sw = sigma1_of<B>(w, q, tile);
+        load_block_rows<B>(a.osrc + pos.frame * a.frame_stride, a.W, pos, q, a.aligned, w);
+        so = sigma1_of<B>(w, q, tile);
+    }
     // :285 under numpy-2 NEP 50: (f32 - f32) / f32(alpha) in f32; :288-289 clip, *255 in f64, trunc
     const float e = (sw - so) / a.alpha32;
     double d = (double)e;
