@@ -302,3 +302,89 @@ def test_empty_and_degenerate(dev):
     with pytest.raises(NotImplementedError):
         batch.embed_batch(torch.zeros((1, 14, 14, 3), dtype=torch.uint8, device=dev),
                           torch.zeros((2, 2), dtype=torch.uint8, device=dev), 7, 0.1)
+
+
+# ---------------------------------------------------------------- SURVEY 4 build-plan items, BASELINE configs
+def test_logical_shards_single_gpu(dev):
+    """8 logical shards on one GPU (dist.shard_range arithmetic, no RCCL):
+    embedding each shard separately equals embedding the whole batch."""
+    from thatsmyface_amd import batch
+    from thatsmyface_amd.dist import ShardedRoundTrip, shard_range
+
+    n, h, w, b = 11, 136, 248, 8
+    frames = batch.synth_frames(n, h, w, seed=0x51A9D, device=dev)
+    tile = batch.synth_tile(h // b, w // b, device=dev)
+    whole = batch.embed_batch(frames, tile, b, 0.1)
+    whole_x = batch.extract_batch(whole, frames, b, 0.1)
+    for world in (8, 3):
+        for rank in range(world):
+            s, e = shard_range(n, rank, world)
+            rt = ShardedRoundTrip(
+                embed_fn=lambda f, t, bb, a, o: batch.embed_batch(f, t, bb, a, out=o),
+                extract_fn=lambda w_, o_, bb, a, out: batch.extract_batch(w_, o_, bb, a, out=out),
+                frames=frames[s:e].contiguous(), tile=tile.clone(), block=b, alpha=0.1)
+            rt.step()
+            assert torch.equal(rt.out, whole[s:e]) and torch.equal(rt.tiles, whole_x[s:e]), (world, rank)
+
+
+def test_call_site_patterns(dev, monkeypatch):
+    """the four call sites, verbatim argument patterns, through the
+    reference-path module, with settings from st.session_state (custom_settings == {})."""
+    import io
+    import sys
+    import types
+
+    class SessionState(dict):  # streamlit's SessionStateProxy: `in` and attribute access
+        def __getattr__(self, k):
+            return self[k]
+
+    st = types.ModuleType("streamlit")
+    st.session_state = SessionState(custom_settings={})
+    monkeypatch.setitem(sys.modules, "streamlit", st)
+    from thatsmyface_amd.modules import watermarking as MW
+
+    rng = np.random.default_rng(77)
+    img = Image.fromarray(rng.integers(0, 256, (200, 264, 3), dtype=np.uint8))
+    qr = Image.fromarray((rng.integers(0, 2, (37, 37)) * 255).astype(np.uint8), "L")
+    buf = io.BytesIO()
+    qr.save(buf, format="PNG")
+    watermark_data = buf.getvalue()
+    a = MW.embed_watermark(img, watermark_data, preserve_ratio=True)  # embed_watermark_page.py:529-531
+    b_ = MW.embed_watermark(img, watermark_data, True)  # watermarking_embed_test.py:102
+    assert np.array_equal(np.asarray(a), np.asarray(b_))
+    tile = O.prepare_tile(np.asarray(qr), 200 // 8, 264 // 8, True)
+    assert np.array_equal(np.asarray(a), O.embed_frame(np.asarray(img), tile, 8, 0.1))
+    x1 = MW.extract_watermark(a, img)  # extract_watermark_page.py:293-296, watermarking_extract_test.py:62
+    assert x1.mode == "L" and x1.size == (264 // 8, 200 // 8)
+    assert np.array_equal(np.asarray(x1), O.extract_frame(np.asarray(a), np.asarray(img), 8, 0.1))
+
+
+def test_config1_batch_256_1080p(dev):
+    """BASELINE configs[1]: 256 x 1080p RGB, b = 8 embed on one GPU -- sampled frames
+    bit-exact against the oracle, the rest deterministic across two launches."""
+    from thatsmyface_amd import batch
+
+    n, h, w, b = 256, 1080, 1920, 8
+    frames = batch.synth_frames(n, h, w, seed=0xC0A1, device=dev)
+    tile = batch.synth_tile(h // b, w // b, device=dev)
+    out = batch.embed_batch(frames, tile, b, 0.1)
+    assert torch.equal(out, batch.embed_batch(frames, tile, b, 0.1))
+    t = tile.cpu().numpy()
+    for f in (0, 97, 255):
+        assert np.array_equal(out[f].cpu().numpy(), O.embed_frame(frames[f].cpu().numpy(), t, b, 0.1)), f
+
+
+@pytest.mark.parametrize("alpha", [0.01, 0.05, 0.1, 0.15, 0.2])
+def test_config4_b16_alpha_sweep_4k(dev, alpha):
+    """BASELINE configs[4]: 16 x 16 blocks, alpha sweep 0.01-0.2 on a 4K frame."""
+    from thatsmyface_amd import batch
+
+    h, w, b = 2160, 3840, 16
+    frames = batch.synth_frames(1, h, w, seed=0xA1F + int(alpha * 100), device=dev)
+    tile = batch.synth_tile(h // b, w // b, device=dev)
+    out = batch.embed_batch(frames, tile, b, alpha)
+    ext = batch.extract_batch(out, frames, b, alpha)
+    host, t = frames[0].cpu().numpy(), tile.cpu().numpy()
+    ref = O.embed_frame(host, t, b, alpha)
+    assert np.array_equal(out[0].cpu().numpy(), ref)
+    assert np.array_equal(ext[0].cpu().numpy(), O.extract_frame(ref, host, b, alpha))
