@@ -69,6 +69,24 @@ def cpu_baseline(host_frames, host_tile, block, alpha):
     }
 
 
+def measured_copy_peak(torch, dev, nbytes=4 << 30, reps=5):
+    """Device-to-device copy rate (read + write bytes / time) of a 4 GiB buffer: the
+    measured stream-copy peak SURVEY 8(d) asks to quote beside the 8 TB/s spec."""
+    src = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    dst = torch.empty_like(src)
+    dst.copy_(src)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        dst.copy_(src)
+    e1.record()
+    e1.synchronize()
+    gbs = 2 * nbytes * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    del src, dst
+    torch.cuda.empty_cache()
+    return round(gbs, 1)
+
+
 def main():
     args = parse()
     import torch
@@ -145,6 +163,8 @@ def main():
         except (OSError, ValueError):
             traffic = None
 
+    copy_gbs = measured_copy_peak(torch, dev) if rank == 0 else None
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_frames > 0:
         k = min(args.cpu_frames, F)
@@ -183,6 +203,8 @@ def main():
                 "traffic": traffic,
                 "algorithmic_bytes_per_launch": embed_bytes,
                 "launch_ms": round(embed_ms, 3),
+                "copy_peak_measured_GBs": copy_gbs,
+                "binding_bound": "VALU issue (DESIGN.md section 4), not HBM",
             },
             "kernels_ms": {"embed": round(embed_ms, 3), "extract": round(extract_ms, 3),
                            "extract_GBs": round(extract_bytes / (extract_ms * 1e-3) / 1e9, 2)},
