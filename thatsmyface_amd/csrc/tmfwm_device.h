@@ -57,13 +57,17 @@ TMF_DEVI uint32_t u8_from_unit(float f)
 }
 
 // ycbcr_to_rgb for one pixel (watermarking.py:55-73): Cb, Cr -= 0.5 in f32, then the
-// dgemv pattern fma(Ti[c][2], cr, fma(Ti[c][0], y, Ti[c][1]*cb)) in f64.
+// dgemv pattern fma(Ti[c][2], cr, fma(Ti[c][0], y, Ti[c][1]*cb)) in f64.  Two terms
+// of it are exact no-ops and are dropped: with Ti[0][1] = 0, fma(1, y, 0*cb) is y up
+// to the sign of a zero, and with Ti[2][2] = 0, fma(0, cr, t) is t up to the sign of
+// a zero; a zero of either sign leaves u8_from_unit at 0, so the bytes are the same
+// for every input (checked over all 2^24 colours by the GPU colour-table test).
 TMF_DEVI void colour_inv(float y, float cbs, float crs, uint32_t &R, uint32_t &G, uint32_t &B)
 {
     const double Y = y, CB = cbs - 0.5f, CR = crs - 0.5f;
-    R = u8_from_unit((float)__builtin_fma(1.403, CR, __builtin_fma(1.0, Y, 0.0 * CB)));
-    G = u8_from_unit((float)__builtin_fma(-0.714, CR, __builtin_fma(1.0, Y, -0.344 * CB)));
-    B = u8_from_unit((float)__builtin_fma(0.0, CR, __builtin_fma(1.0, Y, 1.773 * CB)));
+    R = u8_from_unit((float)__builtin_fma(1.403, CR, Y));
+    G = u8_from_unit((float)__builtin_fma(-0.714, CR, Y + -0.344 * CB));
+    B = u8_from_unit((float)(Y + 1.773 * CB));
 }
 
 // ---------------------------------------------------------------------------
@@ -706,6 +710,23 @@ TMF_DEVI T group_bcast(T v)
     else return swz<(K << 5) | 0x18>(v);                                                // bitmask: (lane & 0x18) | K
 }
 
+// OR over the L lanes of a group (same butterfly as group_sum)
+template <int L>
+TMF_DEVI int group_or(int v)
+{
+    if constexpr (L >= 2) v = v | dpp<0xB1>(v);
+    if constexpr (L >= 4) v = v | dpp<0x4E>(v);
+    if constexpr (L >= 8) v = v | dpp<0x141>(v);
+    return v;
+}
+
+// exec-style mask of the lanes that are member K of their group
+template <int L, int K>
+constexpr unsigned long long kMemberMask = L == 1 ? ~0ull
+                                         : L == 2 ? 0x5555555555555555ull << K
+                                         : L == 4 ? 0x1111111111111111ull << K
+                                                  : 0x0101010101010101ull << K;
+
 TMF_DEVI double fma_t(double a, double b, double c) { return __builtin_fma(a, b, c); }
 TMF_DEVI float fma_t(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
 TMF_DEVI double abs_t(double a) { return __builtin_fabs(a); }
@@ -752,18 +773,41 @@ TMF_DEVI double rsqrt_n(double x)
     }
     return y;
 }
+#ifndef TMF_RSQF_ITERS
+#define TMF_RSQF_ITERS 3
+#endif
 TMF_DEVI float rsqrt_n(float x)
 {
     const unsigned i = 0x5f375a86u - (__builtin_bit_cast(unsigned, x) >> 1);
     float y = __builtin_bit_cast(float, i);
     const float hx = 0.5f * x;
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
+    for (int k = 0; k < TMF_RSQF_ITERS; ++k) {
         const float t = y * y;
         const float u = __builtin_fmaf(-hx, t, 1.5f);
         y = y * u;
     }
     return y;
+}
+
+// Columns i, j of A (and V) <- (c x - s y, s x + c y) as fma(-s, y, c*x), fma(s, x, c*y)
+template <int R, int B, bool WANT_V, typename T>
+TMF_DEVI void rotate_cols(T (&A)[R][B], T (&V)[R][B], int i, int j, T c, T sn)
+{
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const T x = A[r][i], y = A[r][j];
+        A[r][i] = fma_t(-sn, y, c * x);
+        A[r][j] = fma_t(sn, x, c * y);
+    }
+    if constexpr (WANT_V) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const T x = V[r][i], y = V[r][j];
+            V[r][i] = fma_t(-sn, y, c * x);
+            V[r][j] = fma_t(sn, x, c * y);
+        }
+    }
 }
 
 template <typename T>
@@ -826,7 +870,7 @@ TMF_DEVI int jacobi(T (&A)[(B + L - 1) / L][B], T (&V)[(B + L - 1) / L][B], int 
     for (int sweep = 0; sweep < P::kMaxSweeps; ++sweep) {
         T nrm[B];
         static_for<B>([&](auto K) { nrm[K] = cdot<R, B, L>(A, K, K); });
-        int rotated = 0;
+        int rotated = 0;  // this lane rotated one of its own pairs this sweep
         static_for<B - 1>([&](auto S) {
             constexpr int s = S;
             T ga[NP];
@@ -837,7 +881,7 @@ TMF_DEVI int jacobi(T (&A)[(B + L - 1) / L][B], T (&V)[(B + L - 1) / L][B], int 
             // this lane's pairs: select (alpha, beta, gamma), evaluate the rotation test
             // (only here -- the owner's flag travels with its parameters), rotation
             Rot<T> mine[PP];
-            int own_on[PP];
+            unsigned long long own_ball[PP];  // wave mask of the lanes whose U-th pair rotates
             static_for<PP>([&](auto U) {
                 constexpr int p0 = U, i0 = Sched<B>::lo(s, p0), j0 = Sched<B>::hi(s, p0);
                 T a = nrm[i0], b = nrm[j0], g = ga[p0];
@@ -859,7 +903,8 @@ TMF_DEVI int jacobi(T (&A)[(B + L - 1) / L][B], T (&V)[(B + L - 1) / L][B], int 
                 bool skip = g2 <= c2 * (a + b) || g2 <= (P::kTol2 * a) * b;
                 if constexpr (std::is_same_v<T, float>) skip = skip || g2 <= c2a || !live;
                 const bool o = slot != 0 && !skip;
-                own_on[U] = (int)o;
+                own_ball[U] = __ballot(o);
+                rotated |= (int)o;
                 mine[U] = Rot<T>{T(1), T(0), T(0)};
                 if (!kBranchy || __any(o)) {  // wave-uniform: every lane computes, non-rotating lanes keep identity
                     const Rot<T> r = rotation(a, b, g);
@@ -873,34 +918,20 @@ TMF_DEVI int jacobi(T (&A)[(B + L - 1) / L][B], T (&V)[(B + L - 1) / L][B], int 
                 const T c = group_bcast<L, src>(mine[u].c);
                 const T sn = group_bcast<L, src>(mine[u].s);
                 const T tg = group_bcast<L, src>(mine[u].tg);
-                const int on = group_bcast<L, src>(own_on[u]);
-                rotated |= on;
-                // Wave-uniform branch; lanes whose block skips this pair apply the identity
+                // Wave-uniform branch (taken iff the owner lane of this pair rotates it in
+                // some block of the wave); lanes whose block skips this pair apply the identity
                 // (c, s, t*gamma) = (1, 0, 0): fma(-0, y, 1*x) == x bitwise for every value
                 // A (phase 3) and V can hold (their fma chains start from +0 and never make
                 // -0), and A32 / phase-1 A only feed cdot(), which ignores signs of zero.
-                if (!kBranchy || __any(on)) {
+                if (!kBranchy || (own_ball[u] & kMemberMask<L, src>) != 0) {
                     nrm[i] = nrm[i] - tg;
                     nrm[j] = nrm[j] + tg;
-#pragma unroll
-                    for (int r = 0; r < R; ++r) {
-                        const T x = A[r][i], y = A[r][j];
-                        A[r][i] = fma_t(-sn, y, c * x);
-                        A[r][j] = fma_t(sn, x, c * y);
-                    }
-                    if constexpr (WANT_V) {
-#pragma unroll
-                        for (int r = 0; r < R; ++r) {
-                            const T x = V[r][i], y = V[r][j];
-                            V[r][i] = fma_t(-sn, y, c * x);
-                            V[r][j] = fma_t(sn, x, c * y);
-                        }
-                    }
+                    rotate_cols<R, B, WANT_V>(A, V, i, j, c, sn);
                 }
             });
         });
         count += active ? 1 : 0;
-        active = active && rotated;
+        active = active && group_or<L>(rotated) != 0;  // block rotated a pair this sweep
         if (!__any(rotated)) break;
     }
     return count;

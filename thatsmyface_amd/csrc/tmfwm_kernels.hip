@@ -232,37 +232,48 @@ __global__ __launch_bounds__(64) void embed_kernel(EmbedArgs a)
 #pragma unroll
             for (int k = 0; k < B; ++k) U[r][k] = Vf[r][k] = (q * R + r == k) ? 1.0f : 0.0f;
     }
+    // Sort descending (oracle: odd-even transposition sort, stable) as ranks: k goes to
+    // position rk[k] = #{j < k: sig[j] >= sig[k]} + #{j > k: sig[j] > sig[k]}.  The
+    // permutation is applied through LDS: U's columns here, Vt's rows with the B store.
+    int rk[B];
 #pragma unroll
-    for (int round = 0; round < B; ++round)
+    for (int k = 0; k < B; ++k) rk[k] = 0;
 #pragma unroll
-        for (int k = round & 1; k + 1 < B; k += 2) {
-            const bool sw = sig[k] < sig[k + 1];
-            const double s0 = sig[k], s1 = sig[k + 1];
-            sig[k] = sw ? s1 : s0;
-            sig[k + 1] = sw ? s0 : s1;
+    for (int k = 1; k < B; ++k)
 #pragma unroll
-            for (int r = 0; r < R; ++r) {
-                const float u0 = U[r][k], u1 = U[r][k + 1], v0 = Vf[r][k], v1 = Vf[r][k + 1];
-                U[r][k] = sw ? u1 : u0;
-                U[r][k + 1] = sw ? u0 : u1;
-                Vf[r][k] = sw ? v1 : v0;
-                Vf[r][k + 1] = sw ? v0 : v1;
-            }
+        for (int j = 0; j < k; ++j) {
+            const int ge = sig[j] >= sig[k] ? 1 : 0;
+            rk[k] += ge;
+            rk[j] += 1 - ge;
         }
-
-    // N7 blend (:198): S[0] = f32(f64(S[0]) + alpha * (w / 255.0))
-    float S[B];
+    double top = sig[0];
 #pragma unroll
-    for (int k = 0; k < B; ++k) S[k] = (float)sig[k];
-    const uint32_t wv = pos.valid ? a.wm[(int64_t)pos.bi * a.nbw + pos.bj] : 0u;
-    S[0] = (float)((double)S[0] + a.alpha * ((double)wv / 255.0));
+    for (int k = 1; k < B; ++k) top = sig[k] > top ? sig[k] : top;
 
-    // N8 (:201): Bm[k][j] = S'[k] * Vt[k][j] (this lane's rows j of V), then M = U @ Bm
+    // N7 blend (:198): S[0] = f32(f64(S[0]) + alpha * (w / 255.0)), S[0] the largest
+    const uint32_t wv = pos.valid ? a.wm[(int64_t)pos.bi * a.nbw + pos.bj] : 0u;
+    const float s0 = (float)((double)(float)top + a.alpha * ((double)wv / 255.0));
+    float Us[R][B];
 #pragma unroll
     for (int r = 0; r < R; ++r)
         if (real_row<B>(q, r))
 #pragma unroll
-            for (int k = 0; k < B; ++k) tile[k * LD + q * R + r] = S[k] * Vf[r][k];
+            for (int k = 0; k < B; ++k) tile[(q * R + r) * LD + rk[k]] = U[r][k];
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int t = 0; t < B; ++t) Us[r][t] = real_row<B>(q, r) ? tile[(q * R + r) * LD + t] : 0.0f;
+    __syncthreads();
+
+    // N8 (:201): Bm[t][j] = S'[t] * Vt[t][j] (this lane's rows j of V, row t = rank), then M = U @ Bm
+#pragma unroll
+    for (int k = 0; k < B; ++k) {
+        const float sk = rk[k] == 0 ? s0 : (float)sig[k];
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            if (real_row<B>(q, r)) tile[rk[k] * LD + q * R + r] = sk * Vf[r][k];
+    }
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -272,7 +283,7 @@ __global__ __launch_bounds__(64) void embed_kernel(EmbedArgs a)
 #pragma unroll
         for (int k = 0; k < B; ++k)
 #pragma unroll
-            for (int j = 0; j < B; ++j) m[j] = __builtin_fmaf(U[r][k], tile[k * LD + j], m[j]);
+            for (int j = 0; j < B; ++j) m[j] = __builtin_fmaf(Us[r][k], tile[k * LD + j], m[j]);
 #pragma unroll
         for (int j = 0; j < B; ++j) x[r][j] = m[j];
     }
