@@ -48,11 +48,12 @@ TMF_DEVI void chroma(uint32_t R, uint32_t G, uint32_t B, float &cbs, float &crs)
     crs = (float)__builtin_fma(-0.081, b, __builtin_fma(0.5, r, -0.419 * g)) + 0.5f;
 }
 
-// np.clip(.,0,1) in f32, * 255 in f32, astype(uint8) = truncation (watermarking.py:70-73)
+// np.clip(.,0,1) in f32, * 255 in f32, astype(uint8) = truncation (watermarking.py:70-73).
+// The clip is one v_med3_f32; it differs from np.clip only in the sign of a zero
+// result (and on NaN, which no finite pixel produces), and -0 * 255 truncates to 0 too.
 TMF_DEVI uint32_t u8_from_unit(float f)
 {
-    f = f < 0.0f ? 0.0f : f;
-    f = f > 1.0f ? 1.0f : f;
+    f = __builtin_amdgcn_fmed3f(f, 0.0f, 1.0f);
     return (uint32_t)(f * 255.0f);
 }
 
