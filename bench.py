@@ -44,6 +44,9 @@ def parse():
     p.add_argument("--cpu-frames", type=int, default=48,
                    help="frames in the CPU-baseline sample, ~10 s of oracle work on 16 cores (0 = skip)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                   help="process-group backend for N > 1 (nccl = RCCL over xGMI; gloo only to rehearse "
+                        "several ranks on one GPU)")
     return p.parse_args()
 
 
@@ -95,11 +98,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+    # one GPU per rank; more ranks than GPUs only in a gloo rehearsal (ranks share a GPU)
+    gpu = local % max(1, torch.cuda.device_count()) if args.backend == "gloo" else local
+    dev = torch.device("cuda", gpu)
     torch.cuda.set_device(dev)
+    if world > 1:
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     from thatsmyface_amd import batch
     from thatsmyface_amd.dist import ShardedRoundTrip, max_over_ranks, shard_range
@@ -191,7 +198,7 @@ def main():
                 "width": W,
                 "block": b,
                 "alpha": alpha,
-                "parallelism": f"frame shards x{world}, RCCL tile broadcast",
+                "parallelism": f"frame shards x{world}, {'RCCL' if args.backend == 'nccl' else 'gloo'} tile broadcast",
             },
             "roofline": {
                 "bound": "hbm",

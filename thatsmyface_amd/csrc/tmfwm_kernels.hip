@@ -181,8 +181,18 @@ TMF_DEVI void luma_rows(const uint32_t (&words)[Geo<B>::R][Geo<B>::NW], float (&
 // ---------------------------------------------------------------------------
 // Embed: watermarking.py:163-216 fused, one launch per batch.
 // ---------------------------------------------------------------------------
+#ifndef TMF_EMBED_WAVES_BIG
+#define TMF_EMBED_WAVES_BIG 2
+#endif
+// Waves per SIMD the register allocation must allow (1 = unconstrained: the compiler
+// then fits b <= 10 and 14 into 2-3 waves, but b = 12 and 16 overflow into AGPRs and run
+// one wave per SIMD).  Forcing 2 for b = 12 / 16 costs 156 / 256 B of scratch per lane
+// and is faster: embed<12> 283 -> 201 us, embed<16> 531 -> 345 us per 4K frame.
 template <int B>
-__global__ __launch_bounds__(64) void embed_kernel(EmbedArgs a)
+constexpr int kEmbedWaves = (B == 12 || B == 16) ? TMF_EMBED_WAVES_BIG : 1;
+
+template <int B>
+__global__ __launch_bounds__(64, kEmbedWaves<B>) void embed_kernel(EmbedArgs a)
 {
     constexpr int L = Geo<B>::L, R = Geo<B>::R, BPW = Geo<B>::BPW, LD = B + 1, NW = Geo<B>::NW;
     __shared__ float lds[BPW * B * LD];

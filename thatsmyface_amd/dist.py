@@ -35,7 +35,12 @@ def broadcast_tile(tile: torch.Tensor, src: int = 0) -> torch.Tensor:
     """Make every rank's `tile` equal to rank `src`'s (in place)."""
     _, ws = world()
     if ws > 1:
-        dist.broadcast(tile, src=src)
+        if tile.is_cuda and dist.get_backend() == "gloo":  # gloo rehearsal: stage through the host
+            host = tile.cpu()
+            dist.broadcast(host, src=src)
+            tile.copy_(host)
+        else:
+            dist.broadcast(tile, src=src)
     return tile
 
 
@@ -43,6 +48,8 @@ def max_over_ranks(x: float, device: torch.device | str = "cpu") -> float:
     _, ws = world()
     if ws == 1:
         return x
+    if dist.get_backend() == "gloo":
+        device = "cpu"
     t = torch.tensor([x], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
