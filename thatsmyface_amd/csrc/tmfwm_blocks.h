@@ -1,0 +1,332 @@
+// Shared device code of the watermark kernels (gfx950): byte-row I/O, the LDS-mediated
+// 2-D transforms and the fused embed kernel template.  Included by tmfwm_kernels.hip
+// (every other instantiation, the extract kernels and the launchers) and by
+// tmfwm_embed8.hip, which instantiates embed_kernel<8> -- the benchmark's kernel -- in a
+// TU of its own so that it can be scheduled for ILP (Makefile) without the register
+// growth that scheduler costs the other block sizes.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "tmfwm_device.h"
+#include "tmfwm_internal.h"
+
+namespace tmf {
+
+// Opt-in phase profile (make stamps): per-wave s_memtime deltas summed per phase.
+#ifdef TMF_STAMPS
+__device__ unsigned long long g_stamps[16];
+struct Stamp {
+    unsigned long long *t;
+    TMF_DEVI void operator()(int k) const
+    {
+        const unsigned long long now = __builtin_amdgcn_s_memtime();
+        if ((threadIdx.x & 63) == 0 && (blockIdx.x & 63) == 0) atomicAdd(&g_stamps[k], now - *t);  // 1/64 of the waves
+        *t = now;
+    }
+};
+#define TMF_STAMP_INIT unsigned long long tmf_t0 = __builtin_amdgcn_s_memtime(); const Stamp stamp{&tmf_t0}
+#else
+using Stamp = NoStamp;
+#define TMF_STAMP_INIT const Stamp stamp{}
+#endif
+
+// Lanes per block L (== oracle jac_chunks): a power of two for the DPP butterflies,
+// with R = ceil(B/L) rows per lane (rows past B are zero padding).
+template <int B>
+struct Geo {
+    static constexpr int L = B == 4 ? 1 : B <= 8 ? 2 : B <= 12 ? 4 : 8;
+    static constexpr int R = kRows<B, L>;          // rows per lane
+    static constexpr int BPW = 64 / L;             // blocks per wave
+    static constexpr int NBYTES = B * 3;           // bytes per pixel row of a block
+    static constexpr int NW = (NBYTES + 3) / 4;    // u32 words holding them
+    static constexpr bool WORDS = NBYTES % 4 == 0; // dword I/O possible (b = 4, 8, 12, 16)
+};
+static_assert(Geo<6>::L == 2 && Geo<10>::L == 4 && Geo<14>::L == 8 && Geo<14>::R == 2, "lane layout");
+
+// ---- byte rows: dword I/O when the row segment is whole dwords and aligned,
+// otherwise bytes (b = 6, 10, 14: 18, 30, 42 bytes per row)
+template <int B>
+TMF_DEVI void load_words(const uint8_t *p, bool aligned, uint32_t (&w)[Geo<B>::NW])
+{
+    constexpr int NW = Geo<B>::NW, NB = Geo<B>::NBYTES;
+    if (Geo<B>::WORDS && aligned) {
+        const uint32_t *q = reinterpret_cast<const uint32_t *>(p);
+#pragma unroll
+        for (int i = 0; i < NW; ++i) w[i] = q[i];
+    } else {
+#pragma unroll
+        for (int i = 0; i < NW; ++i) {
+            uint32_t v = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (4 * i + k < NB) v |= (uint32_t)p[4 * i + k] << (8 * k);
+            w[i] = v;
+        }
+    }
+}
+
+template <int B>
+TMF_DEVI void store_words(uint8_t *p, bool aligned, const uint32_t (&w)[Geo<B>::NW])
+{
+    constexpr int NW = Geo<B>::NW, NB = Geo<B>::NBYTES;
+    if (Geo<B>::WORDS && aligned) {
+        uint32_t *q = reinterpret_cast<uint32_t *>(p);
+#pragma unroll
+        for (int i = 0; i < NW; ++i) q[i] = w[i];
+    } else {
+#pragma unroll
+        for (int i = 0; i < NW; ++i)
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (4 * i + k < NB) p[4 * i + k] = (uint8_t)(w[i] >> (8 * k));
+    }
+}
+
+TMF_DEVI uint32_t byte_at(const uint32_t *w, int k) { return (w[k >> 2] >> (8 * (k & 3))) & 0xFFu; }
+
+// ---- LDS-mediated 2-D transforms on a block held in rows layout ---------------
+// tile: this block's [B][B+1] LDS region.  x: this lane's R rows.  Column pass
+// first (axis 0), then rows (watermarking.py:76-83).
+template <int B>
+TMF_DEVI bool real_row(int q, int r) { return Geo<B>::R * Geo<B>::L == B || q * Geo<B>::R + r < B; }
+
+template <int B, bool INVERSE>
+TMF_DEVI void dct2d_rows_layout(float (&x)[Geo<B>::R][B], float *tile, int q)
+{
+    constexpr int R = Geo<B>::R, LD = B + 1;
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+        if (real_row<B>(q, r))
+#pragma unroll
+            for (int c = 0; c < B; ++c) tile[(q * R + r) * LD + c] = x[r][c];
+    __syncthreads();
+    // column pass: this lane takes columns [q*R, q*R+R) that exist
+#pragma unroll
+    for (int cc = 0; cc < R; ++cc) {
+        if (!real_row<B>(q, cc)) continue;
+        float col[B];
+#pragma unroll
+        for (int r = 0; r < B; ++r) col[r] = tile[r * LD + q * R + cc];
+        if constexpr (INVERSE) dct::dct3<B>(col); else dct::dct2<B>(col);
+#pragma unroll
+        for (int r = 0; r < B; ++r) tile[r * LD + q * R + cc] = col[r];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        float row[B];
+#pragma unroll
+        for (int c = 0; c < B; ++c) row[c] = real_row<B>(q, r) ? tile[(q * R + r) * LD + c] : 0.0f;
+        if constexpr (INVERSE) dct::dct3<B>(row); else dct::dct2<B>(row);
+#pragma unroll
+        for (int c = 0; c < B; ++c) x[r][c] = real_row<B>(q, r) ? row[c] : 0.0f;
+    }
+    __syncthreads();
+}
+
+struct StripPos {
+    int64_t frame;
+    int bi, bj;
+    bool valid;
+};
+
+template <int B>
+TMF_DEVI StripPos strip_pos(int strips_per_row, int nbw)
+{
+    StripPos p;
+    const int strip = blockIdx.x % strips_per_row;
+    p.bi = blockIdx.x / strips_per_row;
+    p.frame = blockIdx.y;
+    const int g = (threadIdx.x & 63) / Geo<B>::L;
+    p.bj = strip * Geo<B>::BPW + g;
+    p.valid = p.bj < nbw;
+    return p;
+}
+
+// Load this lane's R pixel rows of its block (garbage-free zeros for blocks past
+// the right edge of the block grid) and return luma rows.
+template <int B>
+TMF_DEVI void load_block_rows(const uint8_t *frame_base, int W, const StripPos &pos, int q, bool aligned,
+                              uint32_t (&words)[Geo<B>::R][Geo<B>::NW])
+{
+    constexpr int R = Geo<B>::R;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        if (pos.valid && real_row<B>(q, r)) {
+            const uint8_t *p = frame_base + ((int64_t)(pos.bi * B + q * R + r) * W + (int64_t)pos.bj * B) * 3;
+            load_words<B>(p, aligned, words[r]);
+        } else {
+#pragma unroll
+            for (int i = 0; i < Geo<B>::NW; ++i) words[r][i] = 0u;
+        }
+    }
+}
+
+template <int B>
+TMF_DEVI void luma_rows(const uint32_t (&words)[Geo<B>::R][Geo<B>::NW], float (&y)[Geo<B>::R][B])
+{
+#pragma unroll
+    for (int r = 0; r < Geo<B>::R; ++r)
+#pragma unroll
+        for (int c = 0; c < B; ++c)
+            y[r][c] = luma(byte_at(words[r], 3 * c), byte_at(words[r], 3 * c + 1), byte_at(words[r], 3 * c + 2));
+}
+
+// ---------------------------------------------------------------------------
+// Embed: watermarking.py:163-216 fused, one launch per batch.
+// ---------------------------------------------------------------------------
+#ifndef TMF_EMBED_WAVES_BIG
+#define TMF_EMBED_WAVES_BIG 2
+#endif
+// Waves per SIMD the register allocation must allow (1 = unconstrained: the compiler
+// then fits b <= 10 and 14 into 2-3 waves, but b = 12 and 16 overflow into AGPRs and run
+// one wave per SIMD).  Forcing 2 for b = 12 / 16 costs 156 / 256 B of scratch per lane
+// and is faster: embed<12> 283 -> 201 us, embed<16> 531 -> 345 us per 4K frame.
+template <int B>
+constexpr int kEmbedWaves = (B == 12 || B == 16) ? TMF_EMBED_WAVES_BIG : 1;
+
+template <int B>
+__global__ __launch_bounds__(64, kEmbedWaves<B>) void embed_kernel(EmbedArgs a)
+{
+    constexpr int L = Geo<B>::L, R = Geo<B>::R, BPW = Geo<B>::BPW, LD = B + 1, NW = Geo<B>::NW;
+    __shared__ float lds[BPW * B * LD];
+    __shared__ uint32_t pix[R * NW][64];  // this lane's source bytes, parked during the SVD
+    const int lane = threadIdx.x & 63, g = lane / L, q = lane % L;
+    float *tile = lds + g * B * LD;
+    const StripPos pos = strip_pos<B>(a.strips_per_row, a.nbw);
+    const uint8_t *src = a.src + pos.frame * a.frame_stride;
+    uint8_t *dst = a.dst + pos.frame * a.frame_stride;
+
+    TMF_STAMP_INIT;
+    float x[R][B];
+    {
+        uint32_t words[R][NW];
+        load_block_rows<B>(src, a.W, pos, q, a.aligned, words);
+        luma_rows<B>(words, x);
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int i = 0; i < NW; ++i) pix[r * NW + i][lane] = words[r][i];
+    }
+    dct2d_rows_layout<B, false>(x, tile, q);  // :192
+    stamp(0);
+
+    double A[R][B], V[R][B];
+    svd3<B, L>(x, A, V, q, stamp);  // :195 (SVD)
+
+    // singular values, U = A / sigma, sort descending (oracle orc_svd_block)
+    double sig[B];
+    float U[R][B], Vf[R][B];
+#pragma unroll
+    for (int k = 0; k < B; ++k) sig[k] = cdot_part<R, B>(A, k, k);
+#pragma unroll
+    for (int k = 0; k < B; ++k) {
+        sig[k] = __builtin_sqrt(group_sum<L>(sig[k]));
+        const double inv = 1.0 / sig[k];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            U[r][k] = sig[k] == 0.0 ? 0.0f : (float)(A[r][k] * inv);
+            Vf[r][k] = (float)V[r][k];
+        }
+    }
+    bool zero = true;
+#pragma unroll
+    for (int k = 0; k < B; ++k) zero = zero && (sig[k] == 0.0);
+    if (zero) {  // N6: D == 0 -> U = I, Vt = I
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int k = 0; k < B; ++k) U[r][k] = Vf[r][k] = (q * R + r == k) ? 1.0f : 0.0f;
+    }
+    // Sort descending (oracle: odd-even transposition sort, stable) as ranks: k goes to
+    // position rk[k] = #{j < k: sig[j] >= sig[k]} + #{j > k: sig[j] > sig[k]}.  The
+    // permutation is applied through LDS: U's columns here, Vt's rows with the B store.
+    int rk[B];
+#pragma unroll
+    for (int k = 0; k < B; ++k) rk[k] = 0;
+#pragma unroll
+    for (int k = 1; k < B; ++k)
+#pragma unroll
+        for (int j = 0; j < k; ++j) {
+            const int ge = sig[j] >= sig[k] ? 1 : 0;
+            rk[k] += ge;
+            rk[j] += 1 - ge;
+        }
+    double top = sig[0];
+#pragma unroll
+    for (int k = 1; k < B; ++k) top = sig[k] > top ? sig[k] : top;
+
+    // N7 blend (:198): S[0] = f32(f64(S[0]) + alpha * (w / 255.0)), S[0] the largest
+    const uint32_t wv = pos.valid ? a.wm[(int64_t)pos.bi * a.nbw + pos.bj] : 0u;
+    const float s0 = (float)((double)(float)top + a.alpha * ((double)wv / 255.0));
+    float Us[R][B];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+        if (real_row<B>(q, r))
+#pragma unroll
+            for (int k = 0; k < B; ++k) tile[(q * R + r) * LD + rk[k]] = U[r][k];
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int t = 0; t < B; ++t) Us[r][t] = real_row<B>(q, r) ? tile[(q * R + r) * LD + t] : 0.0f;
+    __syncthreads();
+
+    // N8 (:201): Bm[t][j] = S'[t] * Vt[t][j] (this lane's rows j of V, row t = rank), then M = U @ Bm
+#pragma unroll
+    for (int k = 0; k < B; ++k) {
+        const float sk = rk[k] == 0 ? s0 : (float)sig[k];
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            if (real_row<B>(q, r)) tile[rk[k] * LD + q * R + r] = sk * Vf[r][k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        float m[B];
+#pragma unroll
+        for (int j = 0; j < B; ++j) m[j] = 0.0f;
+#pragma unroll
+        for (int k = 0; k < B; ++k)
+#pragma unroll
+            for (int j = 0; j < B; ++j) m[j] = __builtin_fmaf(Us[r][k], tile[k * LD + j], m[j]);
+#pragma unroll
+        for (int j = 0; j < B; ++j) x[r][j] = m[j];
+    }
+    __syncthreads();
+    stamp(4);
+    dct2d_rows_layout<B, true>(x, tile, q);  // :204
+    stamp(5);
+
+    // :207-216 write back and ycbcr_to_rgb with this lane's original chroma
+    if (pos.valid) {
+        uint32_t words[R][NW];
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int i = 0; i < NW; ++i) words[r][i] = pix[r * NW + i][lane];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            uint32_t out[Geo<B>::NW];
+#pragma unroll
+            for (int i = 0; i < Geo<B>::NW; ++i) out[i] = 0u;
+#pragma unroll
+            for (int c = 0; c < B; ++c) {
+                float cbs, crs;
+                chroma(byte_at(words[r], 3 * c), byte_at(words[r], 3 * c + 1), byte_at(words[r], 3 * c + 2), cbs, crs);
+                uint32_t R8, G8, B8;
+                colour_inv(x[r][c], cbs, crs, R8, G8, B8);
+                const int k0 = 3 * c;
+                out[k0 >> 2] |= R8 << (8 * (k0 & 3));
+                out[(k0 + 1) >> 2] |= G8 << (8 * ((k0 + 1) & 3));
+                out[(k0 + 2) >> 2] |= B8 << (8 * ((k0 + 2) & 3));
+            }
+            uint8_t *p = dst + ((int64_t)(pos.bi * B + q * R + r) * a.W + (int64_t)pos.bj * B) * 3;
+            if (real_row<B>(q, r)) store_words<B>(p, a.aligned, out);
+        }
+    }
+    stamp(6);
+}
+
+}  // namespace tmf

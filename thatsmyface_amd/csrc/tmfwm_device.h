@@ -735,15 +735,23 @@ TMF_DEVI float abs_t(float a) { return __builtin_fabsf(a); }
 TMF_DEVI double sign1_t(double d) { return __builtin_copysign(1.0, d); }
 TMF_DEVI float sign1_t(float d) { return __builtin_copysignf(1.0f, d); }
 
-// sum over rows of A[:,i]*A[:,j] in the contract order (oracle cdot / cdotf)
-template <int R, int B, int L, typename T>
-TMF_DEVI T cdot(const T (&A)[R][B], int i, int j)
+// this lane's part of sum over rows of A[:,i]*A[:,j] (fma chain over its R rows)
+template <int R, int B, typename T>
+TMF_DEVI T cdot_part(const T (&A)[R][B], int i, int j)
 {
     T acc = T(0);
 #pragma unroll
     for (int r = 0; r < R; ++r) acc = fma_t(A[r][i], A[r][j], acc);
-    return group_sum<L>(acc);
+    return acc;
 }
+
+// sum over rows of A[:,i]*A[:,j] in the contract order (oracle cdot / cdotf)
+template <int R, int B, int L, typename T>
+TMF_DEVI T cdot(const T (&A)[R][B], int i, int j)
+{
+    return group_sum<L>(cdot_part<R, B>(A, i, j));
+}
+
 
 // Bitwise blend with an opaque lane mask: keeps the selection a v_bfi_b32 on values,
 // so the optimiser cannot turn "pick nrm[i] by lane" into a dynamically indexed
@@ -870,15 +878,19 @@ TMF_DEVI int jacobi(T (&A)[(B + L - 1) / L][B], T (&V)[(B + L - 1) / L][B], int 
     bool active = live;
     for (int sweep = 0; sweep < P::kMaxSweeps; ++sweep) {
         T nrm[B];
-        static_for<B>([&](auto K) { nrm[K] = cdot<R, B, L>(A, K, K); });
+        // batches of dot products: all lane-local chains first, then all cross-lane sums,
+        // so that the chains interleave and no DPP read waits on the write just before it
+        static_for<B>([&](auto K) { nrm[K] = cdot_part<R, B>(A, K, K); });
+        static_for<B>([&](auto K) { nrm[K] = group_sum<L>(nrm[K]); });
         int rotated = 0;  // this lane rotated one of its own pairs this sweep
         static_for<B - 1>([&](auto S) {
             constexpr int s = S;
             T ga[NP];
             static_for<NP>([&](auto Pi) {
                 constexpr int p = Pi, i = Sched<B>::lo(s, p), j = Sched<B>::hi(s, p);
-                ga[p] = cdot<R, B, L>(A, i, j);
+                ga[p] = cdot_part<R, B>(A, i, j);
             });
+            static_for<NP>([&](auto Pi) { ga[Pi] = group_sum<L>(ga[Pi]); });
             // this lane's pairs: select (alpha, beta, gamma), evaluate the rotation test
             // (only here -- the owner's flag travels with its parameters), rotation
             Rot<T> mine[PP];
@@ -969,11 +981,18 @@ TMF_DEVI void bjorck(double (&V)[(B + L - 1) / L][B])
         return;
     }
     double N[B * (B + 1) / 2];  // packed upper triangle, row j: N[j][k], k >= j
+    static_for<B>([&](auto J) {     // lane-local chains first, cross-lane sums after (cdot)
+        constexpr int j = J;
+        static_for<B - j>([&](auto K0) {
+            constexpr int k = j + K0, idx = j * B - j * (j - 1) / 2 + K0;
+            N[idx] = cdot_part<R, B>(V, j, k);
+        });
+    });
     static_for<B>([&](auto J) {
         constexpr int j = J;
         static_for<B - j>([&](auto K0) {
             constexpr int k = j + K0, idx = j * B - j * (j - 1) / 2 + K0;
-            const double qv = cdot<R, B, L>(V, j, k);
+            const double qv = group_sum<L>(N[idx]);
             N[idx] = (j == k) ? __builtin_fma(-0.5, qv, 1.5) : -0.5 * qv;
         });
     });

@@ -8,10 +8,11 @@ C=$ROOT/thatsmyface_amd/csrc
 T=$(mktemp -d)
 F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -fno-slp-vectorize -Wall $*"
 /opt/rocm/bin/hipcc $F -c "$C/tmfwm_kernels.hip" -o "$T/k.o" &
+/opt/rocm/bin/hipcc $F -mllvm -amdgpu-sched-strategy=max-ilp -c "$C/tmfwm_embed8.hip" -o "$T/e8.o" &
 /opt/rocm/bin/hipcc $F -x hip -c "$C/tmfwm_capi.cpp" -o "$T/c.o" &
 /opt/rocm/bin/hipcc $F -c "$C/tmfwm_tile.hip" -o "$T/t.o" &
 wait
 mkdir -p "$ROOT/variants"
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$ROOT/variants/libtmfwm_$NAME.so" "$T/k.o" "$T/c.o" "$T/t.o"
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$ROOT/variants/libtmfwm_$NAME.so" "$T/k.o" "$T/e8.o" "$T/c.o" "$T/t.o"
 rm -rf "$T"
 echo "variants/libtmfwm_$NAME.so"
