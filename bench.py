@@ -170,6 +170,21 @@ def main():
         except (OSError, ValueError):
             traffic = None
 
+    # VALU-issue bound per frame (tools/valu.py: PMC instruction mix x measured issue costs)
+    valu = {}
+    vp = os.path.join(ROOT, "profiles", "valu.json")
+    if os.path.exists(vp) and H == 2160 and W == 3840:
+        try:
+            with open(vp) as f:
+                vk = json.load(f).get("kernels", {})
+            for name, ms in ((f"embed_kernel<{b}>", embed_ms), (f"extract_kernel<{b}>", extract_ms)):
+                if name in vk:
+                    bound = vk[name]["valu_issue_bound_us_per_frame"]
+                    got = ms * 1e3 / F
+                    valu[name] = {"bound_us_per_frame": bound, "us_per_frame": round(got, 2), "frac": round(bound / got, 3)}
+        except (OSError, ValueError, KeyError):
+            valu = {}
+
     copy_gbs = measured_copy_peak(torch, dev) if rank == 0 else None
 
     cpu = None
@@ -212,9 +227,11 @@ def main():
                 "launch_ms": round(embed_ms, 3),
                 "copy_peak_measured_GBs": copy_gbs,
                 "binding_bound": "VALU issue (DESIGN.md section 4), not HBM",
+                "valu_issue": valu.get(f"embed_kernel<{b}>"),
             },
             "kernels_ms": {"embed": round(embed_ms, 3), "extract": round(extract_ms, 3),
-                           "extract_GBs": round(extract_bytes / (extract_ms * 1e-3) / 1e9, 2)},
+                           "extract_GBs": round(extract_bytes / (extract_ms * 1e-3) / 1e9, 2),
+                           "extract_valu_issue": valu.get(f"extract_kernel<{b}>")},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -11,5 +11,5 @@ P3="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_L
 i=0
 for P in "$P1" "$P2" "$P3"; do
   i=$((i+1))
-  TMFWM_LIB=$LIB timeout -k 10 120 rocprofv3 --pmc $P -d "$OUT/p$i" -o p --output-format csv -- python3 "$GRAFT_REPO_ROOT/tools/time_embed.py" --frames 16 --reps 1 > "$OUT/p$i.log" 2>&1
+  TMFWM_LIB=$LIB timeout -k 10 120 rocprofv3 --pmc $P -d "$OUT/p$i" -o p --output-format csv -- python3 "${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}/tools/time_embed.py" --frames 16 --reps 1 > "$OUT/p$i.log" 2>&1
 done
