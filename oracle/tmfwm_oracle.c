@@ -851,7 +851,9 @@ static int jacobi(double *A, double *V, int b, int want_v)
     return sweep;
 }
 
-/* Phase 3 of the SVD with a first-order finish.  The first sweep is a
+/* NOT CALLED: the device side of this variant measured 7 % slower (DESIGN.md section 9,
+ * item 1), so orc_svd_block keeps jacobi().  Kept as the restatement of that experiment.
+ * Phase 3 of the SVD with a first-order finish.  The first sweep is a
  * plain Jacobi sweep.  Every later sweep starts by computing, from the current A, the
  * couplings gamma of all pairs and, for the pairs the sweep would rotate (the tests of
  * jacobi()), theta = gamma / (beta - alpha) (IEEE division: the small-angle limit of the
