@@ -1,75 +1,142 @@
 #!/usr/bin/env python3
-"""Benchmark: Mpixels/s of the embed+extract round trip on a batch of 4K RGB frames.
+"""Benchmark: Mpixels/s of the embed+extract round trip on a batch of RGB frames.
 
 BASELINE.json metric "Mpixels/s embed+extract, 4K RGB batch, 1/2/4/8 MI355X; % HBM
-roofline", workload configs[2]: 4096 synthetic 3840x2160 RGB frames per GPU, b=8,
-alpha=0.1, embed then extract (watermarking.py:135 and :224 per frame).
+roofline".  Default workload = configs[2]: 4096 synthetic 3840x2160 RGB frames per GPU,
+b=8, alpha=0.1, embed then extract (watermarking.py:135 and :224 per frame).  At
+--gpus 8 the same per-GPU batch is configs[3] (32,768 frames over 8 GPUs).
 
 One step = (rank 0 broadcasts the watermark tile over RCCL when N > 1) + one embed
-launch over the whole batch + one extract launch over the whole batch.  Frames are
-generated in HBM before timing (SURVEY 8(d) generator); nothing crosses PCIe in the
-timed region.  N > 1: one process per GPU (torch.distributed.run), weak scaling
-(every rank processes its own `--frames` frames), no data-path collective besides
-the tile broadcast; value = all ranks' pixels / max-over-ranks time.
+launch over the rank's whole shard + one extract launch over it.  Frames are generated
+in HBM before timing (SURVEY 8(d) generator); nothing crosses PCIe in the timed region.
+
+N > 1: one process per GPU.  Under torch.distributed.run (RANK/WORLD_SIZE in the env)
+this process is one rank; started as `bench.py --gpus N` without them, it launches N
+ranks itself (a child `python -m torch.distributed.run`, started before this process
+touches a GPU) and exits with their status.  Weak scaling: every rank processes its own
+`--frames` frames, a contiguous range of the global batch (thatsmyface_amd.dist);
+value = all ranks' pixels / max-over-ranks time.  Ranks must sit on distinct GPUs
+(checked by PCI id) unless `--backend gloo` rehearses several ranks on one GPU.
 
 Prints ONE JSON line on rank 0.  `roofline` is the embed kernel (the dominant one):
 algorithmic bytes per launch / its mean launch time from HIP events on the launch
 stream.  `cpu_baseline` times the oracle (oracle/, a C port of the reference's
-arithmetic) on a bounded sample on this host's cores.
+arithmetic) on a bounded sample on this host's cores; the same sample's oracle outputs
+are compared with the timed batch's GPU outputs (`parity_sample`), and a mismatch
+makes the run fail.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
+from types import SimpleNamespace
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+BASELINE_METRIC = "Mpixels/s embed+extract, 4K RGB batch, 1/2/4/8 MI355X; % HBM roofline"
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=1)
-    p.add_argument("--frames", type=int, default=4096, help="frames per GPU (configs[2]: 4096)")
+    p.add_argument("--frames", type=int, default=4096, help="frames per GPU (configs[2]/[3]: 4096)")
     p.add_argument("--height", type=int, default=2160)
     p.add_argument("--width", type=int, default=3840)
     p.add_argument("--block", type=int, default=8)
     p.add_argument("--alpha", type=float, default=0.1)
     p.add_argument("--cpu-frames", type=int, default=48,
-                   help="frames in the CPU-baseline sample, ~10 s of oracle work on 16 cores (0 = skip)")
+                   help="frames in the CPU-baseline / parity sample, ~10-20 s of oracle work on 16 cores (0 = skip)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                    help="process-group backend for N > 1 (nccl = RCCL over xGMI; gloo only to rehearse "
                         "several ranks on one GPU)")
-    return p.parse_args()
+    return p.parse_args(argv)
 
 
-def cpu_baseline(host_frames, host_tile, block, alpha):
-    """Oracle (C restatement, OpenMP over block rows) on a bounded sample, this host's cores."""
+def workload_name(F, H, W, b, alpha, world):
+    """Which BASELINE.json config a run is (configs[0] is the CPU-only plumbing case)."""
+    if (H, W) == (2160, 3840) and F == 4096 and b == 8 and world == 8:
+        return "configs[3]: 32768-frame 4K batch over 8 GPUs"
+    if (H, W) == (2160, 3840) and F == 4096 and b == 8 and world == 1:
+        return "configs[2]: 4096 x 4K frames, embed+extract round trip, 1 GPU"
+    if (H, W) == (2160, 3840) and b == 16:
+        return f"configs[4]-style: {F} x 4K frames per GPU, b=16, alpha={alpha}"
+    if (H, W) == (1080, 1920) and b == 8 and F == 256 and world == 1:
+        return "configs[1]: 256 x 1080p frames, 1 GPU"
+    return f"custom: {F} x {W}x{H} frames per GPU x {world}, b={b}, alpha={alpha}"
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(args, argv, script=None) -> int:
+    """Launch args.gpus ranks of this script under torch.distributed.run and return their
+    exit status.  Runs before this process makes any GPU call (device_count does not
+    initialise HIP); the ranks are children, never an exec of this process."""
+    import torch
+
+    if args.backend == "nccl":
+        ndev = torch.cuda.device_count()
+        if ndev < args.gpus:
+            print(f"bench.py: --gpus {args.gpus} needs {args.gpus} visible GPUs, this box has {ndev} "
+                  "(use --backend gloo to rehearse several ranks on one GPU)", file=sys.stderr, flush=True)
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", script or os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def gpu_kernels():
+    """The product path: libtmfwm.so's HIP kernels (thatsmyface_amd.batch)."""
+    from thatsmyface_amd import batch
+
+    return SimpleNamespace(
+        synth_frames=lambda n, h, w, frame0, dev: batch.synth_frames(n, h, w, seed=batch.SEED_COVER, frame0=frame0, device=dev),
+        synth_tile=lambda nbh, nbw, dev: batch.synth_tile(nbh, nbw, device=dev),
+        embed=lambda f, t, b, a, o: batch.embed_batch(f, t, b, a, out=o),
+        extract=lambda w_, o_, b, a, out: batch.extract_batch(w_, o_, b, a, out=out),
+    )
+
+
+def oracle_check(host_frames, host_tile, out, tiles, block, alpha, threads):
+    """Oracle (C restatement, OpenMP) on k frames: (seconds, embed mismatches, extract mismatches).
+    The checker and the CPU baseline are the same computation, timed once."""
+    import numpy as np
+
+    from oracle import oracle as O
+
+    O.lib()
+    t0 = time.perf_counter()
+    emb = O.embed_batch(host_frames, host_tile, block, alpha, threads)
+    ext = O.extract_batch(emb, host_frames, block, alpha, threads)
+    dt = time.perf_counter() - t0
+    bad_e = int(sum(not np.array_equal(emb[i], out[i]) for i in range(len(emb))))
+    bad_x = int(sum(not np.array_equal(ext[i], tiles[i]) for i in range(len(ext))))
+    return dt, bad_e, bad_x
+
+
+def oracle_threads(world: int) -> int:
     from oracle import oracle as O
 
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or O.default_threads()
     threads = max(1, min(threads, O.default_threads()))
-    O.lib()
-    n, h, w = host_frames.shape[:3]
-    t0 = time.perf_counter()
-    emb = O.embed_batch(host_frames, host_tile, block, alpha, threads)
-    O.extract_batch(emb, host_frames, block, alpha, threads)
-    dt = time.perf_counter() - t0
-    return {
-        "value": n * h * w / dt / 1e6,
-        "unit": "Mpixels/s",
-        "cores": threads,
-        "kind": "port",
-        "sample": f"{n} synthetic {w}x{h} frames (the batch's first {n}), embed+extract round trip, "
-                  f"oracle/tmfwm_oracle.c with {threads} OpenMP threads, {dt:.2f} s",
-    }
+    return max(1, threads // max(1, world)) if world > 1 else threads
 
 
 def measured_copy_peak(torch, dev, nbytes=4 << 30, reps=5):
@@ -90,114 +157,189 @@ def measured_copy_peak(torch, dev, nbytes=4 << 30, reps=5):
     return round(gbs, 1)
 
 
-def main():
-    args = parse()
+def _device_id(torch, dev):
+    if dev.type != "cuda":
+        return f"cpu:{socket.gethostname()}"
+    p = torch.cuda.get_device_properties(dev)
+    return f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x} {p.uuid}"
+
+
+def _profile_json(name):
+    path = os.path.join(ROOT, "profiles", name)
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return None
+
+
+def lib_build_id():
+    """sha256 prefix of the loaded libtmfwm.so: profiles/*.json record the build they measured."""
+    import hashlib
+
+    from thatsmyface_amd import _lib
+
+    try:
+        with open(_lib.LIB_PATH, "rb") as f:
+            return hashlib.sha256(f.read()).hexdigest()[:16]
+    except OSError:
+        return None
+
+
+def run(args, kernels=None, device=None):
+    """One rank of the benchmark.  `kernels` / `device` default to the HIP path on this
+    rank's GPU; the CPU test of the multi-rank code substitutes its own (tests/)."""
     import torch
     import torch.distributed as dist
+
+    from thatsmyface_amd.dist import ShardedRoundTrip, max_over_ranks, shard_range
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # one GPU per rank; more ranks than GPUs only in a gloo rehearsal (ranks share a GPU)
-    gpu = local % max(1, torch.cuda.device_count()) if args.backend == "gloo" else local
-    dev = torch.device("cuda", gpu)
-    torch.cuda.set_device(dev)
+    if world > 1 and args.gpus != world:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    if device is None:
+        ndev = torch.cuda.device_count()
+        if ndev == 0:
+            raise SystemExit("bench.py: no GPU visible (the product path has no CPU fallback)")
+        if args.backend == "nccl" and local >= ndev:
+            raise SystemExit(f"bench.py: local rank {local} has no GPU of its own ({ndev} visible)")
+        gpu = local % ndev  # gloo rehearsal: ranks may share a GPU
+        device = torch.device("cuda", gpu)
+        torch.cuda.set_device(device)
+    dev = device
+    on_gpu = dev.type == "cuda"
     if world > 1:
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group("gloo")
+    K = kernels or gpu_kernels()
+    sync = torch.cuda.synchronize if on_gpu else (lambda: None)
 
-    from thatsmyface_amd import batch
-    from thatsmyface_amd.dist import ShardedRoundTrip, max_over_ranks, shard_range
+    # distinct physical devices across ranks
+    ids = [_device_id(torch, dev)]
+    if world > 1:
+        ids = [None] * world
+        dist.all_gather_object(ids, _device_id(torch, dev))
+    n_phys = len(set(ids))
+    if on_gpu and args.backend == "nccl" and n_phys != world:
+        raise SystemExit(f"bench.py: {world} ranks share {n_phys} GPUs ({ids}); RCCL needs one GPU per rank")
 
     F, H, W, b, alpha = args.frames, args.height, args.width, args.block, args.alpha
     nbh, nbw = H // b, W // b
     start, stop = shard_range(F * world, rank, world)  # weak scaling: F frames per GPU
-    frames = batch.synth_frames(stop - start, H, W, seed=batch.SEED_COVER, frame0=start, device=dev)
-    wm = batch.synth_tile(nbh, nbw, device=dev) if rank == 0 else torch.zeros((nbh, nbw), dtype=torch.uint8, device=dev)
-    torch.cuda.synchronize()
+    frames = K.synth_frames(stop - start, H, W, start, dev)
+    wm = K.synth_tile(nbh, nbw, dev) if rank == 0 else torch.zeros((nbh, nbw), dtype=torch.uint8, device=dev)
+    sync()
 
-    stream = torch.cuda.current_stream()
     marks = {}
+    if on_gpu:
+        stream = torch.cuda.current_stream()
 
-    def hook(phase):
-        e = torch.cuda.Event(enable_timing=True)
-        e.record(stream)
-        marks.setdefault(phase, []).append(e)
+        def hook(phase):
+            e = torch.cuda.Event(enable_timing=True)
+            e.record(stream)
+            marks.setdefault(phase, []).append(e)
+    else:
+        def hook(phase):
+            marks.setdefault(phase, []).append(time.perf_counter())
 
-    rt = ShardedRoundTrip(
-        embed_fn=lambda f, t, bb, a, o: batch.embed_batch(f, t, bb, a, out=o),
-        extract_fn=lambda w_, o_, bb, a, out: batch.extract_batch(w_, o_, bb, a, out=out),
-        frames=frames, tile=wm, block=b, alpha=alpha,
-    )
+    rt = ShardedRoundTrip(embed_fn=K.embed, extract_fn=K.extract, frames=frames, tile=wm, block=b, alpha=alpha)
 
     for _ in range(args.warmup):
         rt.step()
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     rt.hooks.append(hook)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         rt.step()
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     elapsed = max_over_ranks(time.perf_counter() - t0, dev)
     ev = list(zip(marks["broadcast"], marks["embed"], marks["extract"]))
-
-    embed_ms = sum(a.elapsed_time(m) for a, m, _ in ev) / len(ev)
-    extract_ms = sum(m.elapsed_time(z) for _, m, z in ev) / len(ev)
+    if on_gpu:
+        embed_ms = sum(a.elapsed_time(m) for a, m, _ in ev) / len(ev)
+        extract_ms = sum(m.elapsed_time(z) for _, m, z in ev) / len(ev)
+    else:
+        embed_ms = sum(m - a for a, m, _ in ev) / len(ev) * 1e3
+        extract_ms = sum(z - m for _, m, z in ev) / len(ev) * 1e3
     px_step = F * H * W * world
     value = px_step * args.steps / elapsed / 1e6
 
-    embed_bytes = F * (6 * H * W + nbh * nbw)  # read 3HW + nh*nw, write 3HW per frame
-    extract_bytes = F * (6 * H * W + nbh * nbw)  # read 6HW, write nh*nw per frame
+    # SURVEY 8(d) algorithmic bytes per frame
+    embed_read, embed_write = 3 * H * W + nbh * nbw, 3 * H * W
+    embed_bytes = F * (embed_read + embed_write)
+    extract_bytes = F * (6 * H * W + nbh * nbw)
     achieved = embed_bytes / (embed_ms * 1e-3) / 1e9
+    achieved_read = F * embed_read / (embed_ms * 1e-3) / 1e9
+
+    # parity of the timed batch against the oracle: rank 0 at N = 1 checks the CPU-baseline
+    # sample (its first k frames); at N > 1 every rank checks the last frame of its shard
+    cpu, parity = None, None
+    n_local = stop - start
+    want_cpu = rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_frames > 0
+    checked = bad_e = bad_x = 0
+    if want_cpu or (world > 1 and n_local > 0):
+        idx = list(range(min(args.cpu_frames, n_local))) if want_cpu else [n_local - 1]
+        threads = oracle_threads(world)
+        host = frames[idx].cpu().numpy()
+        dt, bad_e, bad_x = oracle_check(host, wm.cpu().numpy(), rt.out[idx].cpu().numpy(),
+                                        rt.tiles[idx].cpu().numpy(), b, alpha, threads)
+        checked = len(idx)
+        if want_cpu:
+            cpu = {
+                "value": round(checked * H * W / dt / 1e6, 3),
+                "unit": "Mpixels/s",
+                "cores": threads,
+                "kind": "port",
+                "sample": f"{checked} synthetic {W}x{H} frames (the batch's first {checked}), embed+extract round trip, "
+                          f"oracle/tmfwm_oracle.c with {threads} OpenMP threads, {dt:.2f} s",
+            }
+    if world > 1:  # every rank joins, checked or not
+        cdev = dev if args.backend == "nccl" else "cpu"
+        counts = torch.tensor([checked, bad_e, bad_x], dtype=torch.int64, device=cdev)
+        dist.all_reduce(counts)
+        checked, bad_e, bad_x = (int(v) for v in counts.cpu())
+    if checked:
+        parity = {"frames": checked, "embed_mismatch": bad_e, "extract_mismatch": bad_x,
+                  "summary": f"{checked - max(bad_e, bad_x)}/{checked} frames bit-exact vs oracle"}
+
+    copy_gbs = measured_copy_peak(torch, dev) if rank == 0 and on_gpu else None
+    build = lib_build_id() if on_gpu else None
 
     traffic = None
-    tp = os.path.join(ROOT, "profiles", "traffic.json")
-    if os.path.exists(tp):
-        try:
-            with open(tp) as f:
-                tj = json.load(f)
-            key = f"{F}x{H}x{W}_b{b}"
-            if key in tj.get("embed_kernel_hbm_bytes_per_launch", {}):
-                traffic = tj["embed_kernel_hbm_bytes_per_launch"][key]
-        except (OSError, ValueError):
-            traffic = None
+    tj = _profile_json("traffic.json")
+    if tj and (tj.get("build_id") in (None, build)):
+        traffic = tj.get("embed_kernel_hbm_bytes_per_launch", {}).get(f"{F}x{H}x{W}_b{b}")
 
-    # VALU-issue bound per frame (tools/valu.py: PMC instruction mix x measured issue costs)
     valu = {}
-    vp = os.path.join(ROOT, "profiles", "valu.json")
-    if os.path.exists(vp) and H == 2160 and W == 3840:
-        try:
-            with open(vp) as f:
-                vk = json.load(f).get("kernels", {})
-            for name, ms in ((f"embed_kernel<{b}>", embed_ms), (f"extract_kernel<{b}>", extract_ms)):
-                if name in vk:
-                    bound = vk[name]["valu_issue_bound_us_per_frame"]
-                    got = ms * 1e3 / F
-                    valu[name] = {"bound_us_per_frame": bound, "us_per_frame": round(got, 2), "frac": round(bound / got, 3)}
-        except (OSError, ValueError, KeyError):
-            valu = {}
-
-    copy_gbs = measured_copy_peak(torch, dev) if rank == 0 else None
-
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_frames > 0:
-        k = min(args.cpu_frames, F)
-        cpu = cpu_baseline(frames[:k].cpu().numpy(), wm.cpu().numpy(), b, alpha)
+    vj = _profile_json("valu.json")
+    if vj and H == 2160 and W == 3840 and vj.get("build_id") == build:
+        for name, ms in ((f"embed_kernel<{b}>", embed_ms), (f"extract_kernel<{b}>", extract_ms)):
+            k = vj.get("kernels", {}).get(name)
+            if k:
+                bound = k["valu_issue_bound_us_per_frame"]
+                got = ms * 1e3 / F
+                valu[name] = {"bound_us_per_frame": bound, "us_per_frame": round(got, 2),
+                              "issue_fraction": round(bound / got, 3), "clock_MHz": k.get("clock_MHz")}
 
     if rank == 0:
+        is4k = (H, W) == (2160, 3840)
         line = {
-            "metric": "Mpixels/s embed+extract, 4K RGB batch",
+            "metric": BASELINE_METRIC if is4k else f"Mpixels/s embed+extract, {W}x{H} RGB batch",
             "value": round(value, 3),
             "unit": "Mpixels/s",
-            "n_gpus": world,
+            "n_gpus": n_phys if on_gpu else 0,
+            "n_ranks": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3),
@@ -207,13 +349,15 @@ def main():
             "dtype": "f64+f32 (u8 I/O)",
             "data": "synthetic (splitmix64 uniform u8 covers + tile, generated in HBM)",
             "config": {
-                "workload": f"{F} x {W}x{H} RGB frames per GPU, embed+extract round trip (configs[2])",
+                "workload": workload_name(F, H, W, b, alpha, world),
                 "frames_per_gpu": F,
+                "frames_total": F * world,
                 "height": H,
                 "width": W,
                 "block": b,
                 "alpha": alpha,
-                "parallelism": f"frame shards x{world}, {'RCCL' if args.backend == 'nccl' else 'gloo'} tile broadcast",
+                "parallelism": ("single GPU" if world == 1 else
+                                f"frame shards x{world}, {'RCCL' if args.backend == 'nccl' else 'gloo'} tile broadcast"),
             },
             "roofline": {
                 "bound": "hbm",
@@ -223,6 +367,8 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5),
                 "traffic": traffic,
+                "read_achieved": round(achieved_read, 2),
+                "read_frac": round(achieved_read / HBM_PEAK_GBS, 5),
                 "algorithmic_bytes_per_launch": embed_bytes,
                 "launch_ms": round(embed_ms, 3),
                 "copy_peak_measured_GBs": copy_gbs,
@@ -232,12 +378,28 @@ def main():
             "kernels_ms": {"embed": round(embed_ms, 3), "extract": round(extract_ms, 3),
                            "extract_GBs": round(extract_bytes / (extract_ms * 1e-3) / 1e9, 2),
                            "extract_valu_issue": valu.get(f"extract_kernel<{b}>")},
+            "parity_sample": parity,
             "cpu_baseline": cpu,
+            "lib_build": build,
         }
+        if world > 1 and args.backend == "gloo":
+            line["rehearsal"] = f"gloo: {world} ranks on {n_phys} device(s); not a multi-GPU measurement"
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    if parity and (parity["embed_mismatch"] or parity["extract_mismatch"]):
+        print(f"bench.py: parity FAILED on rank {rank}: {parity}", file=sys.stderr, flush=True)
+        return 3
+    return 0
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return spawn_ranks(args, argv)
+    return run(args)
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

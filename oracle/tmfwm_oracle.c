@@ -851,101 +851,6 @@ static int jacobi(double *A, double *V, int b, int want_v)
     return sweep;
 }
 
-/* NOT CALLED: the device side of this variant measured 7 % slower (DESIGN.md section 9,
- * item 1), so orc_svd_block keeps jacobi().  Kept as the restatement of that experiment.
- * Phase 3 of the SVD with a first-order finish.  The first sweep is a
- * plain Jacobi sweep.  Every later sweep starts by computing, from the current A, the
- * couplings gamma of all pairs and, for the pairs the sweep would rotate (the tests of
- * jacobi()), theta = gamma / (beta - alpha) (IEEE division: the small-angle limit of the
- * rotation's t = tan).  No pair to rotate: converged (exactly jacobi()'s sweep without a
- * rotation).  Every such pair with theta^4 * alpha_max <= 2^-112 * min(alpha, beta):
- * the rotations left are so small that c = 1 - theta^2/2 and the cross terms between
- * pairs stay below 2^-56 of the smaller column, so the sweep becomes the shears
- * a_i -= theta a_j, a_j += theta a_i (old values of the pair; pairs in schedule order;
- * A and V alike) and the phase ends.  Otherwise a plain Jacobi sweep follows.  Returns
- * the sweeps done, the first-order sweep included. */
-#define JAC_FO_T 1.925929944387236e-34 /* 2^-112 */
-static int jacobi_fo(double *A, double *V, int b)
-{
-    int sweep;
-    double F = 0.0, nrm[ORC_MAXB], th[ORC_MAXB * ORC_MAXB];
-    for (int k = 0; k < b; ++k) F += cdot(A + k, A + k, b, b);
-    const double c2 = JAC_C2 * F;
-    for (sweep = 0; sweep < JAC_MAX_SWEEPS; ++sweep) {
-        for (int k = 0; k < b; ++k) nrm[k] = cdot(A + k, A + k, b, b);
-        if (sweep > 0) {
-            double amax = nrm[0];
-            for (int k = 1; k < b; ++k) amax = nrm[k] > amax ? nrm[k] : amax;
-            int any = 0, ok = 1;
-            for (int st = 0; st < b - 1; ++st)
-                for (int p = 0; p < b / 2; ++p) {
-                    int i, j;
-                    jac_pairs(b, st, p, &i, &j);
-                    const double alpha = nrm[i], beta = nrm[j];
-                    const double gamma = cdot(A + i, A + j, b, b);
-                    const double g2 = gamma * gamma;
-                    double t = 0.0;
-                    if (!(g2 <= c2 * (alpha + beta) || g2 <= (JAC_TOL2 * alpha) * beta)) {
-                        any = 1;
-                        t = gamma / (beta - alpha);
-                        const double t2 = t * t;
-                        if (!((t2 * t2) * amax <= JAC_FO_T * (alpha < beta ? alpha : beta))) ok = 0;
-                    }
-                    th[st * ORC_MAXB + p] = t;
-                }
-            if (!any) { ++sweep; break; }
-            if (ok) {
-                for (int st = 0; st < b - 1; ++st)
-                    for (int p = 0; p < b / 2; ++p) {
-                        int i, j;
-                        jac_pairs(b, st, p, &i, &j);
-                        const double t = th[st * ORC_MAXB + p];
-                        for (int r = 0; r < b; ++r) {
-                            const double x = A[r * b + i], y = A[r * b + j];
-                            A[r * b + i] = fma(-t, y, x);
-                            A[r * b + j] = fma(t, x, y);
-                        }
-                        for (int r = 0; r < b; ++r) {
-                            const double x = V[r * b + i], y = V[r * b + j];
-                            V[r * b + i] = fma(-t, y, x);
-                            V[r * b + j] = fma(t, x, y);
-                        }
-                    }
-                ++sweep;
-                break;
-            }
-        }
-        int rotated = 0;
-        for (int st = 0; st < b - 1; ++st) {
-            for (int p = 0; p < b / 2; ++p) {
-                int i, j;
-                jac_pairs(b, st, p, &i, &j);
-                const double alpha = nrm[i], beta = nrm[j];
-                const double gamma = cdot(A + i, A + j, b, b);
-                const double g2 = gamma * gamma;
-                if (g2 <= c2 * (alpha + beta) || g2 <= (JAC_TOL2 * alpha) * beta) continue;
-                rotated = 1;
-                double c, sn, tg;
-                rotation(alpha, beta, gamma, &c, &sn, &tg);
-                nrm[i] = alpha - tg;
-                nrm[j] = beta + tg;
-                for (int r = 0; r < b; ++r) {
-                    const double x = A[r * b + i], y = A[r * b + j];
-                    A[r * b + i] = fma(-sn, y, c * x);
-                    A[r * b + j] = fma(sn, x, c * y);
-                }
-                for (int r = 0; r < b; ++r) {
-                    const double x = V[r * b + i], y = V[r * b + j];
-                    V[r * b + i] = fma(-sn, y, c * x);
-                    V[r * b + j] = fma(sn, x, c * y);
-                }
-            }
-        }
-        if (!rotated) { ++sweep; break; }
-    }
-    return sweep;
-}
-
 /* Full SVD of one block: D (b x b f32 row-major) -> U (b x b), S (b), Vt (b x b), f32, sorted descending.
  * Returns the sweeps done: f64 sweeps | (f32 sweeps << 8). */
 int orc_svd_block(const float *D, int b, float *U, float *S, float *Vt)
