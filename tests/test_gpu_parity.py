@@ -388,3 +388,81 @@ def test_config4_b16_alpha_sweep_4k(dev, alpha):
     ref = O.embed_frame(host, t, b, alpha)
     assert np.array_equal(out[0].cpu().numpy(), ref)
     assert np.array_equal(ext[0].cpu().numpy(), O.extract_frame(ref, host, b, alpha))
+
+
+def test_config2_full_batch_4096x4k(dev):
+    """BASELINE configs[2] at full size: 4096 x 4K frames (102 GB in, 102 GB out) in one
+    embed and one extract launch.  First, middle and last frames bit-exact against the
+    oracle; PSNR(watermarked, cover) over the whole batch in the reference's band."""
+    from thatsmyface_amd import batch
+
+    n, h, w, b = 4096, 2160, 3840, 8
+    frames = batch.synth_frames(n, h, w, device=dev)
+    tile = batch.synth_tile(h // b, w // b, device=dev)
+    out = ext = None
+    try:
+        out = batch.embed_batch(frames, tile, b, 0.1)
+        ext = batch.extract_batch(out, frames, b, 0.1)
+        t = tile.cpu().numpy()
+        for f in (0, n // 2, n - 1):
+            host = frames[f].cpu().numpy()
+            ref = O.embed_frame(host, t, b, 0.1)
+            assert np.array_equal(out[f].cpu().numpy(), ref), f
+            assert np.array_equal(ext[f].cpu().numpy(), O.extract_frame(ref, host, b, 0.1)), f
+        sq = 0
+        for s in range(0, n, 128):
+            d = out[s:s + 128].to(torch.int16) - frames[s:s + 128].to(torch.int16)
+            sq += int((d.to(torch.int32) ** 2).sum(dtype=torch.int64).item())
+            del d
+        psnr = 10 * np.log10(255.0 ** 2 / (sq / (n * h * w * 3)))
+        assert 40.0 < psnr < 50.0, psnr
+    finally:
+        del frames, out, ext
+        torch.cuda.empty_cache()
+
+
+def test_threads_dropin_gpu(dev):
+    """Streamlit runs sessions on threads: 8 threads call embed_watermark /
+    extract_watermark at once on different images, sizes and block sizes; every result
+    is checked against the oracle."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from thatsmyface_amd import watermarking as W
+
+    jobs = []
+    for i in range(16):
+        b = ALL_B[i % len(ALL_B)]
+        h, w = 96 + 8 * i, 160 + 12 * i
+        jobs.append((i, b, _u8(100 + i, (h, w, 3)), _u8(200 + i, (13 + i, 17 + i)), 0.05 + 0.01 * i))
+
+    def work(job):
+        i, b, rgb, wm, alpha = job
+        s = {"block_size": b, "alpha": alpha}
+        e = np.asarray(W.embed_watermark(Image.fromarray(rgb), Image.fromarray(wm, "L"), i % 2 == 0, s))
+        x = np.asarray(W.extract_watermark(Image.fromarray(e), Image.fromarray(rgb), s))
+        return e, x
+
+    with ThreadPoolExecutor(8) as ex:
+        res = list(ex.map(work, jobs))
+    for (i, b, rgb, wm, alpha), (e, x) in zip(jobs, res):
+        tile = O.prepare_tile(wm, rgb.shape[0] // b, rgb.shape[1] // b, i % 2 == 0)
+        ref = O.embed_frame(rgb, tile, b, alpha)
+        assert np.array_equal(e, ref), i
+        assert np.array_equal(x, O.extract_frame(ref, rgb, b, alpha)), i
+
+
+def test_overlapping_buffers_refused(dev):
+    """tmfwm_embed / tmfwm_extract refuse output ranges that overlap an input range."""
+    from thatsmyface_amd import _lib
+
+    h, w, b = 32, 32, 8
+    buf = torch.zeros(2 * h * w * 3, dtype=torch.uint8, device=dev)
+    tile = torch.zeros((h // b, w // b), dtype=torch.uint8, device=dev)
+    L = _lib.load()
+    st = torch.cuda.current_stream().cuda_stream
+    with pytest.raises(ValueError, match="overlaps"):  # out starts inside the input frame
+        _lib.check(L.tmfwm_embed(buf.data_ptr(), 1, h, w, h * w * 3, tile.data_ptr(), b, 0.1, buf.data_ptr() + 100,
+                                 _lib.MEM_DEVICE, st), "embed")
+    with pytest.raises(ValueError, match="overlaps"):
+        _lib.check(L.tmfwm_extract(buf.data_ptr(), buf.data_ptr(), 1, h, w, h * w * 3, b, 0.1, buf.data_ptr() + 5,
+                                   _lib.MEM_DEVICE, st), "extract")

@@ -2,7 +2,7 @@
 
 CPU: the oracle stands in for the device stage (test infrastructure only), so the
 decode / ordered-device / encode overlap logic is checked without a GPU.
-GPU: the real stage against the drop-in embed_watermark + PNG per image.
+GPU: the real (HIP) stage against the oracle's prepare_tile + embed_frame + PNG per image.
 """
 import io
 
@@ -58,17 +58,20 @@ def test_pipeline_order_and_png_cpu():
 
 
 @pytest.mark.gpu
-def test_pipeline_matches_dropin_gpu():
+def test_pipeline_matches_oracle_gpu():
+    """The HIP device stage (prepare_tile + embed on the GPU) against the oracle's
+    prepare_tile + embed_frame, and the PNG round trip of the result."""
     torch = pytest.importorskip("torch")
     assert torch.cuda.is_available()
-    from thatsmyface_amd import watermarking as W
 
     imgs, wm = _images(9, seed=5), _wm_png()
+    grey = np.asarray(Image.open(io.BytesIO(wm)).convert("L"))
     for b, pr in ((8, True), (12, False)):
         settings = {"block_size": b, "alpha": 0.15}
         res = pipeline.embed_images(imgs, wm, pr, settings)
         for src, r in zip(imgs, res):
-            img = src if isinstance(src, Image.Image) else Image.open(io.BytesIO(src))
-            ref = np.asarray(W.embed_watermark(img, wm, pr, settings))
+            rgb = pipeline._decode(src)
+            tile = O.prepare_tile(grey, rgb.shape[0] // b, rgb.shape[1] // b, pr)
+            ref = O.embed_frame(rgb, tile, b, 0.15)
             assert np.array_equal(r.pixels, ref), (b, pr)
             assert np.array_equal(np.asarray(Image.open(io.BytesIO(r.png))), ref)

@@ -94,6 +94,13 @@ int need_device()
     return 0;
 }
 
+// [a, a+na) and [b, b+nb) share a byte (the kernels read one while writing the other)
+bool ranges_overlap(const void *a, size_t na, const void *b, size_t nb)
+{
+    const uintptr_t x = reinterpret_cast<uintptr_t>(a), y = reinterpret_cast<uintptr_t>(b);
+    return na && nb && x < y + nb && y < x + na;
+}
+
 size_t span_bytes(int64_t n, int64_t stride, int64_t frame_bytes) { return n == 0 ? 0 : (size_t)((n - 1) * stride + frame_bytes); }
 
 }  // namespace
@@ -141,7 +148,8 @@ int tmfwm_embed(const uint8_t *rgb, int64_t n_frames, int32_t height, int32_t wi
         if (tbytes) {
             if (int rc = check_device_ptr(wm_tile, "wm_tile")) return rc;
         }
-        if ((const void *)rgb == (const void *)out) return fail(TMFWM_ERR_INVALID, "out aliases rgb");
+        if (ranges_overlap(rgb, span, out, span)) return fail(TMFWM_ERR_INVALID, "out overlaps rgb (in-place embed is not supported)");
+        if (tbytes && ranges_overlap(wm_tile, tbytes, out, span)) return fail(TMFWM_ERR_INVALID, "out overlaps wm_tile");
         a.src = rgb;
         a.dst = out;
         a.wm = wm_tile;
@@ -200,6 +208,9 @@ int tmfwm_extract(const uint8_t *wm_rgb, const uint8_t *orig_rgb, int64_t n_fram
         if (int rc = check_device_ptr(wm_rgb, "wm_rgb")) return rc;
         if (int rc = check_device_ptr(orig_rgb, "orig_rgb")) return rc;
         if (int rc = check_device_ptr(out_tiles, "out_tiles")) return rc;
+        const size_t obytes = (size_t)(tbytes * n_frames);
+        if (ranges_overlap(out_tiles, obytes, wm_rgb, span) || ranges_overlap(out_tiles, obytes, orig_rgb, span))
+            return fail(TMFWM_ERR_INVALID, "out_tiles overlaps an input batch");
         a.wsrc = wm_rgb;
         a.osrc = orig_rgb;
         a.out = out_tiles;
