@@ -21,12 +21,13 @@ _lib = None
 _u8p = ctypes.POINTER(ctypes.c_uint8)
 _f32p = ctypes.POINTER(ctypes.c_float)
 _i32p = ctypes.POINTER(ctypes.c_int32)
+_f64p = ctypes.POINTER(ctypes.c_double)
 
 
 def build(force: bool = False) -> str:
     """Compile the oracle with its Makefile (gcc); returns the .so path."""
     if force or not os.path.exists(_LIB_PATH) or (
-        os.path.getmtime(_LIB_PATH) < os.path.getmtime(os.path.join(_HERE, "tmfwm_oracle.c"))
+        os.path.getmtime(_LIB_PATH) < max(os.path.getmtime(os.path.join(_HERE, f)) for f in ("tmfwm_oracle.c", "tmfwm_lapack.c"))
     ):
         subprocess.run(["make", "-s", "-C", _HERE], check=True)
     return _LIB_PATH
@@ -56,6 +57,13 @@ def lib():
             "orc_synth_bytes": (None, [ctypes.c_uint64, I64, I64, I64, _u8p]),
             "orc_resize_lanczos": (I32, [_u8p, I32, I32, I32, I32, _u8p, I32]),
             "orc_prepare_tile": (I32, [_u8p, I32, I32, I32, I32, I32, _u8p]),
+            "orc_embed_frame_mode": (I32, [_u8p, I32, I32, _u8p, I32, D, _u8p, I32, I32, ctypes.POINTER(I64)]),
+            "orc_extract_frame_mode": (I32, [_u8p, _u8p, I32, I32, I32, D, _u8p, I32, I32]),
+            "orc_svd_flag": (I32, [_f64p, I32]),
+            "orc_svd_blocks_f64": (None, [_f32p, I64, I32, _f64p, _f64p, _f64p, I32]),
+            "orc_lp_dnrm2": (D, [I32, _f64p, I32]),
+            "orc_lp_svd_blocks": (I32, [_f32p, I64, I32, _f32p, _f32p, _f32p, I32]),
+            "orc_lp_svd": (I32, [_f64p, I32, _f64p, _f64p, _f64p]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -118,6 +126,50 @@ def svd_blocks(D: np.ndarray):
     return U, S, Vt, sw[:nb]
 
 
+def lp_svd_blocks(D: np.ndarray, nthreads: int | None = None):
+    """numpy.linalg.svd of float32 blocks as the reference gets it (LAPACK dgesdd route,
+    tmfwm_lapack.c): f32 U, S, Vt."""
+    D = np.ascontiguousarray(D, dtype=np.float32)
+    b = D.shape[-1]
+    nb = D.size // (b * b)
+    U = np.empty(D.shape, np.float32)
+    Vt = np.empty(D.shape, np.float32)
+    S = np.empty(D.shape[:-1], np.float32)
+    if lib().orc_lp_svd_blocks(_p(D, _f32p), nb, b, _p(U, _f32p), _p(S, _f32p), _p(Vt, _f32p), nthreads or default_threads()):
+        raise ValueError("lapack restatement did not converge")
+    return U, S, Vt
+
+
+def svd_blocks_f64(D: np.ndarray, nthreads: int | None = None):
+    """The Jacobi route's f64 factors before rounding: U (u[r][k]), sig, V (v[r][k]), sorted."""
+    D = np.ascontiguousarray(D, dtype=np.float32)
+    b = D.shape[-1]
+    nb = D.size // (b * b)
+    U = np.empty(D.shape, np.float64)
+    V = np.empty(D.shape, np.float64)
+    S = np.empty(D.shape[:-1], np.float64)
+    lib().orc_svd_blocks_f64(_p(D, _f32p), nb, b, _p(U, _f64p), _p(S, _f64p), _p(V, _f64p), nthreads or default_threads())
+    return U, S, V
+
+
+def lp_dnrm2(x: np.ndarray, inc: int = 1) -> float:
+    """OpenBLAS dnrm2 (x87 extended, four accumulators) as restated for LAPACK's dlarfg."""
+    x = np.ascontiguousarray(x, np.float64)
+    n = (x.size + inc - 1) // inc if x.size else 0
+    return float(lib().orc_lp_dnrm2(n, _p(x, _f64p), inc))
+
+
+def lp_svd(a: np.ndarray):
+    """numpy.linalg.svd of one f64 n x n matrix (dgesdd route restated): u, s, vt in f64."""
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    n = a.shape[0]
+    u, vt, s = np.empty((n, n)), np.empty((n, n)), np.empty(n)
+    rc = lib().orc_lp_svd(_p(a, _f64p), n, _p(u, _f64p), _p(s, _f64p), _p(vt, _f64p))
+    if rc:
+        raise ValueError(f"lapack restatement rc={rc}")
+    return u, s, vt
+
+
 def sigma1(D: np.ndarray) -> float:
     D = np.ascontiguousarray(D, dtype=np.float32)
     return float(lib().orc_sigma1_block(_p(D, _f32p), D.shape[-1]))
@@ -147,28 +199,53 @@ def blend_reconstruct(U, S, Vt, w: int, alpha: float) -> np.ndarray:
 
 
 # --- whole-frame paths ------------------------------------------------------
-def embed_frame(rgb: np.ndarray, wm_tile: np.ndarray, block: int, alpha: float, nthreads: int | None = None) -> np.ndarray:
+# SVD routes (tmfwm_oracle.c ORC_SVD_*): "lapack" = the reference's own dgesdd arithmetic
+# (tmfwm_lapack.c); "jacobi" / "hybrid" = the specified device routes.  None = the route
+# libtmfwm.so implements (the contract the GPU tests compare against).
+ROUTES = {"jacobi": 0, "lapack": 1, "hybrid": 2}
+
+
+def embed_frame(rgb: np.ndarray, wm_tile: np.ndarray, block: int, alpha: float, nthreads: int | None = None,
+                route: str | None = None, stats: dict | None = None) -> np.ndarray:
     rgb = np.ascontiguousarray(rgb, dtype=np.uint8)
     H, W = rgb.shape[:2]
     wm_tile = np.ascontiguousarray(wm_tile, dtype=np.uint8)
     assert wm_tile.shape == (H // block, W // block), (wm_tile.shape, H, W, block)
     out = np.empty_like(rgb)
-    rc = lib().orc_embed_frame(_p(rgb, _u8p), H, W, _p(wm_tile, _u8p), block, float(alpha), _p(out, _u8p), nthreads or default_threads())
+    nfb = ctypes.c_int64(0)
+    if route is None:
+        rc = lib().orc_embed_frame(_p(rgb, _u8p), H, W, _p(wm_tile, _u8p), block, float(alpha), _p(out, _u8p), nthreads or default_threads())
+    else:
+        rc = lib().orc_embed_frame_mode(_p(rgb, _u8p), H, W, _p(wm_tile, _u8p), block, float(alpha), _p(out, _u8p),
+                                        nthreads or default_threads(), ROUTES[route], ctypes.byref(nfb))
     if rc:
         raise ValueError(f"oracle embed failed rc={rc}")
+    if stats is not None:
+        stats["fallback_blocks"] = int(nfb.value)
     return out
 
 
-def extract_frame(wrgb: np.ndarray, orgb: np.ndarray, block: int, alpha: float, nthreads: int | None = None) -> np.ndarray:
+def extract_frame(wrgb: np.ndarray, orgb: np.ndarray, block: int, alpha: float, nthreads: int | None = None,
+                  route: str | None = None) -> np.ndarray:
     wrgb = np.ascontiguousarray(wrgb, dtype=np.uint8)
     orgb = np.ascontiguousarray(orgb, dtype=np.uint8)
     H, W = wrgb.shape[:2]
     assert orgb.shape == wrgb.shape
     out = np.empty((H // block, W // block), np.uint8)
-    rc = lib().orc_extract_frame(_p(wrgb, _u8p), _p(orgb, _u8p), H, W, block, float(alpha), _p(out, _u8p), nthreads or default_threads())
+    if route is None:
+        rc = lib().orc_extract_frame(_p(wrgb, _u8p), _p(orgb, _u8p), H, W, block, float(alpha), _p(out, _u8p), nthreads or default_threads())
+    else:
+        rc = lib().orc_extract_frame_mode(_p(wrgb, _u8p), _p(orgb, _u8p), H, W, block, float(alpha), _p(out, _u8p),
+                                          nthreads or default_threads(), ROUTES[route])
     if rc:
         raise ValueError(f"oracle extract failed rc={rc}")
     return out
+
+
+def svd_flag(sig: np.ndarray) -> bool:
+    """The hybrid route's conditioning test on one block's f64 singular values."""
+    sig = np.ascontiguousarray(sig, np.float64)
+    return bool(lib().orc_svd_flag(_p(sig, _f64p), sig.size))
 
 
 def embed_batch(rgb: np.ndarray, wm_tile: np.ndarray, block: int, alpha: float, nthreads: int | None = None) -> np.ndarray:

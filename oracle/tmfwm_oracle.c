@@ -35,6 +35,21 @@
 
 #define ORC_MAXB 16
 
+/* SVD routes:
+ *   ORC_SVD_JACOBI  every block through the specified 3-phase Jacobi;
+ *   ORC_SVD_LAPACK  every block through the restated dgesdd route (tmfwm_lapack.c) --
+ *                   the reference's own arithmetic;
+ *   ORC_SVD_HYBRID  Jacobi, except blocks the conditioning test orc_svd_flag()
+ *                   flags, which take the dgesdd route (the device contract). */
+#define ORC_SVD_JACOBI 0
+#define ORC_SVD_LAPACK 1
+#define ORC_SVD_HYBRID 2
+/* the route libtmfwm.so implements (orc_embed_frame / orc_extract_frame) */
+#ifndef ORC_SVD_CONTRACT
+#define ORC_SVD_CONTRACT ORC_SVD_JACOBI
+#endif
+int orc_lp_svd_block_f32(const float *D, int n, float *U, float *S, float *Vt);
+
 /* ------------------------------------------------------------------------ */
 /* N1 / N2: RGB -> YCbCr (watermarking.py:23-50)                            */
 /* ------------------------------------------------------------------------ */
@@ -851,18 +866,19 @@ static int jacobi(double *A, double *V, int b, int want_v)
     return sweep;
 }
 
-/* Full SVD of one block: D (b x b f32 row-major) -> U (b x b), S (b), Vt (b x b), f32, sorted descending.
+/* Full SVD of one block in f64, before rounding: D (b x b f32 row-major) -> U (b x b,
+ * u[r][k]), sig (b), V (b x b, v[r][k]), sorted by descending sig.  Zero block: U = V = I.
  * Returns the sweeps done: f64 sweeps | (f32 sweeps << 8). */
-int orc_svd_block(const float *D, int b, float *U, float *S, float *Vt)
+int orc_svd_block_f64(const float *D, int b, double *U, double *sig, double *V)
 {
-    double A[ORC_MAXB * ORC_MAXB], V[ORC_MAXB * ORC_MAXB], sig[ORC_MAXB];
+    double A[ORC_MAXB * ORC_MAXB];
     int allzero = 1;
     for (int k = 0; k < b * b; ++k) { A[k] = D[k]; if (D[k] != 0.0f) allzero = 0; }
     for (int r = 0; r < b; ++r) for (int k = 0; k < b; ++k) V[r * b + k] = (r == k) ? 1.0 : 0.0;
     if (allzero) {
         /* N6: LAPACK returns U = I, Vt = I for the zero matrix */
-        for (int r = 0; r < b; ++r) for (int k = 0; k < b; ++k) { U[r * b + k] = (r == k); Vt[r * b + k] = (r == k); }
-        for (int k = 0; k < b; ++k) S[k] = 0.0f;
+        for (int r = 0; r < b; ++r) for (int k = 0; k < b; ++k) U[r * b + k] = (r == k);
+        for (int k = 0; k < b; ++k) sig[k] = 0.0;
         return 0;
     }
     /* phase 1: f32 Jacobi on D; phase 2: V0 = Bjorck^2(f64(V32)); phase 3: f64
@@ -879,16 +895,14 @@ int orc_svd_block(const float *D, int b, float *U, float *S, float *Vt)
             A[r * b + k] = acc;
         }
     const int sweeps = jacobi(A, V, b, 1) | (s32 << 8);
-    float Uf[ORC_MAXB * ORC_MAXB], Vf[ORC_MAXB * ORC_MAXB];
     for (int k = 0; k < b; ++k) {
         sig[k] = sqrt(cdot(A + k, A + k, b, b));
         if (sig[k] == 0.0) {
-            for (int r = 0; r < b; ++r) Uf[r * b + k] = 0.0f;
+            for (int r = 0; r < b; ++r) U[r * b + k] = 0.0;
         } else {
             const double inv = 1.0 / sig[k];
-            for (int r = 0; r < b; ++r) Uf[r * b + k] = (float)(A[r * b + k] * inv);
+            for (int r = 0; r < b; ++r) U[r * b + k] = A[r * b + k] * inv;
         }
-        for (int r = 0; r < b; ++r) Vf[r * b + k] = (float)V[r * b + k];
     }
     /* odd-even transposition sort, descending on the f64 singular values */
     for (int round = 0; round < b; ++round)
@@ -896,18 +910,34 @@ int orc_svd_block(const float *D, int b, float *U, float *S, float *Vt)
             if (sig[k] < sig[k + 1]) {
                 double ts = sig[k]; sig[k] = sig[k + 1]; sig[k + 1] = ts;
                 for (int r = 0; r < b; ++r) {
-                    float tu = Uf[r * b + k]; Uf[r * b + k] = Uf[r * b + k + 1]; Uf[r * b + k + 1] = tu;
-                    float tv = Vf[r * b + k]; Vf[r * b + k] = Vf[r * b + k + 1]; Vf[r * b + k + 1] = tv;
+                    double tu = U[r * b + k]; U[r * b + k] = U[r * b + k + 1]; U[r * b + k + 1] = tu;
+                    double tv = V[r * b + k]; V[r * b + k] = V[r * b + k + 1]; V[r * b + k + 1] = tv;
                 }
             }
+    return sweeps;
+}
+
+/* Full SVD of one block: D (b x b f32 row-major) -> U (b x b), S (b), Vt (b x b), f32, sorted descending.
+ * Returns the sweeps done: f64 sweeps | (f32 sweeps << 8). */
+int orc_svd_block(const float *D, int b, float *U, float *S, float *Vt)
+{
+    double U64[ORC_MAXB * ORC_MAXB], V64[ORC_MAXB * ORC_MAXB], sig[ORC_MAXB];
+    const int sweeps = orc_svd_block_f64(D, b, U64, sig, V64);
     for (int k = 0; k < b; ++k) {
         S[k] = (float)sig[k];
-        for (int r = 0; r < b; ++r) { U[r * b + k] = Uf[r * b + k]; Vt[k * b + r] = Vf[r * b + k]; }
+        for (int r = 0; r < b; ++r) { U[r * b + k] = (float)U64[r * b + k]; Vt[k * b + r] = (float)V64[r * b + k]; }
     }
     return sweeps;
 }
 
-/* sigma_1 only (extract path): f32(max_k ||(A V)_k||) */
+void orc_svd_blocks_f64(const float *D, int64_t nb, int b, double *U, double *S, double *V, int nthreads)
+{
+    if (nthreads < 1) nthreads = 1;
+#pragma omp parallel for num_threads(nthreads) schedule(static)
+    for (int64_t k = 0; k < nb; ++k) orc_svd_block_f64(D + k * b * b, b, U + k * b * b, S + k * b, V + k * b * b);
+}
+
+/* sigma_1 only (extract path), Jacobi route: f32(max_k ||(A V)_k||) */
 float orc_sigma1_block(const float *D, int b)
 {
     double A[ORC_MAXB * ORC_MAXB];
@@ -919,6 +949,65 @@ float orc_sigma1_block(const float *D, int b)
         if (s > m) m = s;
     }
     return (float)m;
+}
+
+/* Conditioning test of the hybrid route.  Where the f64 Jacobi and LAPACK part ways in
+ * the last bits, the f32-rounded factors can differ, and with them the reconstructed
+ * block: both methods' factor errors grow like eps * sigma_1 / min(gap_k, sigma_k)
+ * (gap_k = distance of sigma_k to the nearest other singular value).  A block is
+ * flagged when that amplification exceeds 2^20 for any singular triplet that reaches
+ * the output (f32(sigma_k) != 0).  Measured (tests/test_oracle_lapack.py): every
+ * block whose reconstruction differs between the two routes has amplification
+ * >= 6e7; flagged fractions 0.01 % (noise covers) to 0.5 % (camera-like covers).
+ * sig: the f64 singular values of the Jacobi route (any order). */
+#define ORC_FLAG_T 1048576.0 /* 2^20 */
+int orc_svd_flag(const double *sig, int b)
+{
+    double s1 = 0.0;
+    for (int k = 0; k < b; ++k) if (sig[k] > s1) s1 = sig[k];
+    if (s1 == 0.0) return 0; /* zero block: U = V = I exactly on both routes (N6) */
+    double m = s1;
+    for (int k = 0; k < b; ++k) {
+        if ((float)sig[k] == 0.0f) continue;
+        double g = sig[k];
+        for (int j = 0; j < b; ++j) {
+            if (j == k) continue;
+            const double d = fabs(sig[k] - sig[j]);
+            if (d < g) g = d;
+        }
+        if (g < m) m = g;
+    }
+    return m * ORC_FLAG_T < s1;
+}
+
+/* One block's factors by route; returns 1 when the dgesdd route produced them. */
+int orc_svd_block_mode(const float *D, int b, int mode, float *U, float *S, float *Vt)
+{
+    if (mode == ORC_SVD_LAPACK) {
+        orc_lp_svd_block_f32(D, b, U, S, Vt);
+        return 1;
+    }
+    double U64[ORC_MAXB * ORC_MAXB], V64[ORC_MAXB * ORC_MAXB], sig[ORC_MAXB];
+    orc_svd_block_f64(D, b, U64, sig, V64);
+    if (mode == ORC_SVD_HYBRID && orc_svd_flag(sig, b)) {
+        orc_lp_svd_block_f32(D, b, U, S, Vt);
+        return 1;
+    }
+    for (int k = 0; k < b; ++k) {
+        S[k] = (float)sig[k];
+        for (int r = 0; r < b; ++r) { U[r * b + k] = (float)U64[r * b + k]; Vt[k * b + r] = (float)V64[r * b + k]; }
+    }
+    return 0;
+}
+
+/* sigma_1 by route: the Jacobi value, or LAPACK's S[0] (the reference's value; the
+ * device extract certifies it or computes it on the dgesdd route). */
+static float sigma1_mode(const float *D, int b, int mode)
+{
+    if (mode == ORC_SVD_JACOBI) return orc_sigma1_block(D, b);
+    float U[ORC_MAXB * ORC_MAXB], S[ORC_MAXB], Vt[ORC_MAXB * ORC_MAXB];
+    orc_lp_svd_block_f32(D, b, U, S, Vt);
+    return S[0];
 }
 
 /* N7 blend + N8 reconstruct: S'[0] = f32(f64(S0) + alpha*(w/255.0)); M = U @ (diag(S') @ Vt) */
@@ -1006,27 +1095,31 @@ void orc_scatter_blocks(const float *blocks, int H, int W, int b, float *Y)
 }
 
 /* One block row (bi) of the embed: Y plane updated in place. */
-static void embed_block_row(float *Y, int W, int b, int bi, int nbw, const uint8_t *wm, double alpha)
+static int64_t embed_block_row(float *Y, int W, int b, int bi, int nbw, const uint8_t *wm, double alpha, int mode)
 {
+    int64_t fallback = 0;
     const dct_plan *p = plan_for(b);
     float D[ORC_MAXB * ORC_MAXB], U[ORC_MAXB * ORC_MAXB], Vt[ORC_MAXB * ORC_MAXB], S[ORC_MAXB], M[ORC_MAXB * ORC_MAXB];
     for (int bj = 0; bj < nbw; ++bj) {
         for (int r = 0; r < b; ++r)
             for (int c = 0; c < b; ++c) D[r * b + c] = Y[(int64_t)(bi * b + r) * W + bj * b + c];
         dct2d(p, D, 0);                                    /* :192 */
-        orc_svd_block(D, b, U, S, Vt);                     /* :195 */
+        fallback += orc_svd_block_mode(D, b, mode, U, S, Vt); /* :195 */
         orc_blend_reconstruct(U, S, Vt, b, wm[(int64_t)bi * nbw + bj], alpha, M); /* :198-201 */
         dct2d(p, M, 1);                                    /* :204 */
         for (int r = 0; r < b; ++r)
             for (int c = 0; c < b; ++c) Y[(int64_t)(bi * b + r) * W + bj * b + c] = M[r * b + c]; /* :207-210 */
     }
+    return fallback;
 }
 
 static int clamp_threads(int nthreads) { return nthreads < 1 ? 1 : nthreads; }
 
 /* embed_watermark arithmetic for one frame (watermarking.py:163-216).
- * rgb: H x W x 3 u8; wm: (H/b) x (W/b) u8 tile (already resized); out: H x W x 3 u8. */
-int orc_embed_frame(const uint8_t *rgb, int H, int W, const uint8_t *wm, int b, double alpha, uint8_t *out, int nthreads)
+ * rgb: H x W x 3 u8; wm: (H/b) x (W/b) u8 tile (already resized); out: H x W x 3 u8.
+ * mode: ORC_SVD_*; n_fallback (optional) receives the blocks that took the dgesdd route. */
+int orc_embed_frame_mode(const uint8_t *rgb, int H, int W, const uint8_t *wm, int b, double alpha, uint8_t *out,
+                         int nthreads, int mode, int64_t *n_fallback)
 {
     if (!orc_supported_block(b) || H < 0 || W < 0) return -1;
     plans_init();
@@ -1041,18 +1134,26 @@ int orc_embed_frame(const uint8_t *rgb, int H, int W, const uint8_t *wm, int b, 
         Y[q] = ycc[3 * q];
     }
     const int nbh = H / b, nbw = W / b;
-#pragma omp parallel for num_threads(nthreads) schedule(dynamic, 1)
-    for (int bi = 0; bi < nbh; ++bi) embed_block_row(Y, W, b, bi, nbw, wm, alpha);
+    int64_t fallback = 0;
+#pragma omp parallel for num_threads(nthreads) schedule(dynamic, 1) reduction(+ : fallback)
+    for (int bi = 0; bi < nbh; ++bi) fallback += embed_block_row(Y, W, b, bi, nbw, wm, alpha, mode);
 #pragma omp parallel for num_threads(nthreads) schedule(static)
     for (int64_t q = 0; q < npix; ++q) colour_inv(Y[q], ycc[3 * q + 1], ycc[3 * q + 2], out + 3 * q);
     free(ycc);
     free(Y);
+    if (n_fallback) *n_fallback = fallback;
     return 0;
+}
+
+int orc_embed_frame(const uint8_t *rgb, int H, int W, const uint8_t *wm, int b, double alpha, uint8_t *out, int nthreads)
+{
+    return orc_embed_frame_mode(rgb, H, W, wm, b, alpha, out, nthreads, ORC_SVD_CONTRACT, NULL);
 }
 
 /* extract_watermark arithmetic for one frame pair (watermarking.py:241-289).
  * Both images H x W x 3 (the original already cropped to the watermarked size). out: (H/b) x (W/b). */
-int orc_extract_frame(const uint8_t *wrgb, const uint8_t *orgb, int H, int W, int b, double alpha, uint8_t *out, int nthreads)
+int orc_extract_frame_mode(const uint8_t *wrgb, const uint8_t *orgb, int H, int W, int b, double alpha, uint8_t *out,
+                           int nthreads, int mode)
 {
     if (!orc_supported_block(b) || H < 0 || W < 0) return -1;
     plans_init();
@@ -1075,7 +1176,7 @@ int orc_extract_frame(const uint8_t *wrgb, const uint8_t *orgb, int H, int W, in
                 }
             dct2d(p, Dw, 0);
             dct2d(p, Do, 0);
-            const float sw = orc_sigma1_block(Dw, b), so = orc_sigma1_block(Do, b);
+            const float sw = sigma1_mode(Dw, b, mode), so = sigma1_mode(Do, b, mode);
             /* :285 numpy-2 NEP 50: float32 - float32, then / python float in float32 */
             const float e = (sw - so) / alpha32;
             /* :288-289 stored in f64, clip [0,1], *255 (f64), astype(uint8) */
@@ -1086,6 +1187,11 @@ int orc_extract_frame(const uint8_t *wrgb, const uint8_t *orgb, int H, int W, in
         }
     }
     return 0;
+}
+
+int orc_extract_frame(const uint8_t *wrgb, const uint8_t *orgb, int H, int W, int b, double alpha, uint8_t *out, int nthreads)
+{
+    return orc_extract_frame_mode(wrgb, orgb, H, W, b, alpha, out, nthreads, ORC_SVD_CONTRACT);
 }
 
 /* Batched helpers for the CPU baseline (frames laid out back to back). */

@@ -101,7 +101,7 @@ def _cover_image(arr):
 
 
 def test_golden_cases_dropin_gpu(dev, golden):
-    from test_oracle_golden import ILL_CONDITIONED
+    from test_oracle_golden import JACOBI_ILL as ILL_CONDITIONED
 
     from thatsmyface_amd import watermarking as W
 
