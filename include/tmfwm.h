@@ -24,6 +24,12 @@
  * (frame_stride >= height*width*3).  Block grid: nbh = height / block,
  * nbw = width / block.  Supported block sizes: 4, 6, 8, 10, 12, 14, 16 -- the app's
  * slider values (others return TMFWM_ERR_UNSUPPORTED).
+ *
+ * SVD routes: every block goes through a fused Jacobi SVD; the
+ * blocks whose factors could round differently from LAPACK's (conditioning test) are
+ * redone by a second pass on the dgesdd route -- numpy's np.linalg.svd restated
+ * operation by operation (LAPACK 3.12 + OpenBLAS 0.3.29 SkylakeX kernels) -- so the
+ * bytes are the reference's.  The _ex entry points report how many blocks took it.
  */
 #ifndef TMFWM_H
 #define TMFWM_H
@@ -34,7 +40,7 @@
 extern "C" {
 #endif
 
-#define TMFWM_ABI_VERSION 1
+#define TMFWM_ABI_VERSION 2
 
 #define TMFWM_MEM_HOST 0
 #define TMFWM_MEM_DEVICE 1
@@ -66,6 +72,16 @@ int tmfwm_embed(const uint8_t *rgb, int64_t n_frames, int32_t height, int32_t wi
                 const uint8_t *wm_tile, int32_t block, double alpha, uint8_t *out, int32_t mem_kind, void *hip_stream);
 
 /*
+ * tmfwm_embed with a report: *n_lapack_blocks (optional, host pointer) receives the
+ * number of blocks that took the dgesdd route.  Passing it makes the call wait for
+ * `hip_stream` (the count lives on the device); NULL keeps TMFWM_MEM_DEVICE calls
+ * asynchronous.
+ */
+int tmfwm_embed_ex(const uint8_t *rgb, int64_t n_frames, int32_t height, int32_t width, int64_t frame_stride,
+                   const uint8_t *wm_tile, int32_t block, double alpha, uint8_t *out, int32_t mem_kind, void *hip_stream,
+                   int64_t *n_lapack_blocks);
+
+/*
  * Extract: replaces the body of extract_watermark() (watermarking.py:246-292):
  * luma of both images, per-block sigma_1 of the DCT of each, (s_w - s_o)/alpha
  * in float32, clip to [0,1], *255, truncation.  Both images have the same
@@ -75,6 +91,12 @@ int tmfwm_embed(const uint8_t *rgb, int64_t n_frames, int32_t height, int32_t wi
 int tmfwm_extract(const uint8_t *wm_rgb, const uint8_t *orig_rgb, int64_t n_frames, int32_t height, int32_t width,
                   int64_t frame_stride, int32_t block, double alpha, uint8_t *out_tiles, int32_t mem_kind,
                   void *hip_stream);
+
+/* tmfwm_extract with a report: *n_lapack_blocks (optional) receives the number of
+ * blocks whose sigma_1 pair was computed on the dgesdd route (the rest are certified). */
+int tmfwm_extract_ex(const uint8_t *wm_rgb, const uint8_t *orig_rgb, int64_t n_frames, int32_t height, int32_t width,
+                     int64_t frame_stride, int32_t block, double alpha, uint8_t *out_tiles, int32_t mem_kind,
+                     void *hip_stream, int64_t *n_lapack_blocks);
 
 /* rgb_to_ycbcr (watermarking.py:23): npix RGB uint8 pixels -> npix x 3 float32 (Y, Cb+0.5, Cr+0.5). */
 int tmfwm_rgb_to_ycbcr(const uint8_t *rgb, int64_t npix, float *ycc, int32_t mem_kind, void *hip_stream);
@@ -93,6 +115,18 @@ int tmfwm_dct2d_blocks(float *blocks, int64_t n_blocks, int32_t block, int32_t i
  * (0 for an all-zero block). */
 int tmfwm_svd_blocks(const float *D, int64_t n_blocks, int32_t block, float *U, float *S, float *Vt, int32_t *sweeps,
                      int32_t mem_kind, void *hip_stream);
+
+/* np.linalg.svd(D) on the dgesdd route (the reference's own arithmetic, restated for the
+ * GPU): U, S (descending), Vt in float32 for n_blocks row-major blocks.  want_vectors = 0
+ * computes S only (U and Vt may be NULL).  Synchronises `hip_stream`; a block on which
+ * dbdsqr does not converge returns TMFWM_ERR_INVALID. */
+int tmfwm_lapack_svd_blocks(const float *D, int64_t n_blocks, int32_t block, float *U, float *S, float *Vt,
+                            int32_t want_vectors, int32_t mem_kind, void *hip_stream);
+
+/* OpenBLAS dnrm2 as LAPACK's dlarfg sees it (x87 extended arithmetic, emulated): out[v]
+ * = nrm2 of n elements, stride inc, of vector v (vectors n*inc doubles apart). */
+int tmfwm_lapack_nrm2(const double *x, int64_t n_vectors, int32_t n, int32_t inc, double *out, int32_t mem_kind,
+                      void *hip_stream);
 
 /* Synthetic frames generated in device memory (bench inputs):
  * out[f*frame_bytes + i] = splitmix64(seed ^ ((frame0+f) << 40) ^ i) & 0xFF. */

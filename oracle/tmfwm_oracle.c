@@ -46,7 +46,7 @@
 #define ORC_SVD_HYBRID 2
 /* the route libtmfwm.so implements (orc_embed_frame / orc_extract_frame) */
 #ifndef ORC_SVD_CONTRACT
-#define ORC_SVD_CONTRACT ORC_SVD_JACOBI
+#define ORC_SVD_CONTRACT ORC_SVD_HYBRID
 #endif
 int orc_lp_svd_block_f32(const float *D, int n, float *U, float *S, float *Vt);
 

@@ -30,9 +30,20 @@ def _check_frames(t: torch.Tensor, name: str) -> None:
         raise ValueError(f"{name} must be contiguous")
 
 
+def _count_ptr(stats):
+    import ctypes
+
+    if stats is None:
+        return None, None
+    c = ctypes.c_int64(0)
+    return c, ctypes.addressof(c)
+
+
 def embed_batch(frames: torch.Tensor, wm_tile: torch.Tensor, block: int = 8, alpha: float = 0.1,
-                out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
-    """Embed one watermark tile into every frame (watermarking.py:135 per frame)."""
+                out: torch.Tensor | None = None, stream=None, stats: dict | None = None) -> torch.Tensor:
+    """Embed one watermark tile into every frame (watermarking.py:135 per frame).
+    stats (optional dict) receives "lapack_blocks": the blocks redone on the dgesdd route;
+    asking for it synchronises the stream."""
     _check_frames(frames, "frames")
     n, h, w, _ = frames.shape
     if block not in SUPPORTED_BLOCK_SIZES:
@@ -46,16 +57,20 @@ def embed_batch(frames: torch.Tensor, wm_tile: torch.Tensor, block: int = 8, alp
         _check_frames(out, "out")
         if out.shape != frames.shape:
             raise ValueError("out shape mismatch")
+    cnt, ptr = _count_ptr(stats)
     with torch.cuda.device(frames.device):
         L = _lib.load()
-        _lib.check(L.tmfwm_embed(frames.data_ptr(), n, h, w, h * w * 3, wm_tile.data_ptr(), block, float(alpha),
-                                 out.data_ptr(), _lib.MEM_DEVICE, _stream(stream)), "embed_batch")
+        _lib.check(L.tmfwm_embed_ex(frames.data_ptr(), n, h, w, h * w * 3, wm_tile.data_ptr(), block, float(alpha),
+                                    out.data_ptr(), _lib.MEM_DEVICE, _stream(stream), ptr), "embed_batch")
+    if stats is not None:
+        stats["lapack_blocks"] = int(cnt.value)
     return out
 
 
 def extract_batch(wframes: torch.Tensor, oframes: torch.Tensor, block: int = 8, alpha: float = 0.1,
-                  out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
-    """Extract the watermark tile of every frame pair (watermarking.py:224 per pair)."""
+                  out: torch.Tensor | None = None, stream=None, stats: dict | None = None) -> torch.Tensor:
+    """Extract the watermark tile of every frame pair (watermarking.py:224 per pair).
+    stats (optional dict) receives "lapack_blocks" (synchronises the stream)."""
     _check_frames(wframes, "wframes")
     _check_frames(oframes, "oframes")
     if wframes.shape != oframes.shape:
@@ -65,10 +80,13 @@ def extract_batch(wframes: torch.Tensor, oframes: torch.Tensor, block: int = 8, 
         raise NotImplementedError(f"block {block}")
     if out is None:
         out = torch.empty((n, h // block, w // block), dtype=torch.uint8, device=wframes.device)
+    cnt, ptr = _count_ptr(stats)
     with torch.cuda.device(wframes.device):
         L = _lib.load()
-        _lib.check(L.tmfwm_extract(wframes.data_ptr(), oframes.data_ptr(), n, h, w, h * w * 3, block, float(alpha),
-                                   out.data_ptr(), _lib.MEM_DEVICE, _stream(stream)), "extract_batch")
+        _lib.check(L.tmfwm_extract_ex(wframes.data_ptr(), oframes.data_ptr(), n, h, w, h * w * 3, block, float(alpha),
+                                      out.data_ptr(), _lib.MEM_DEVICE, _stream(stream), ptr), "extract_batch")
+    if stats is not None:
+        stats["lapack_blocks"] = int(cnt.value)
     return out
 
 
@@ -109,6 +127,24 @@ def svd_blocks(D: torch.Tensor):
         _lib.check(L.tmfwm_svd_blocks(D.data_ptr(), n, b, U.data_ptr(), S.data_ptr(), Vt.data_ptr(), sw.data_ptr(),
                                       _lib.MEM_DEVICE, _stream(None)), "svd_blocks")
     return U, S, Vt, sw
+
+
+def lapack_svd_blocks(D: torch.Tensor, want_vectors: bool = True):
+    """np.linalg.svd on the dgesdd route (the reference's arithmetic) for (n, b, b) float32
+    blocks on the GPU: (U, S, Vt), or (None, S, None) without vectors."""
+    if not D.is_cuda or D.dtype != torch.float32 or D.dim() != 3 or D.shape[1] != D.shape[2]:
+        raise ValueError("D must be (n, b, b) float32 on the GPU")
+    D = D.contiguous()
+    n, b, _ = D.shape
+    S = torch.empty((n, b), dtype=torch.float32, device=D.device)
+    U = torch.empty_like(D) if want_vectors else None
+    Vt = torch.empty_like(D) if want_vectors else None
+    with torch.cuda.device(D.device):
+        L = _lib.load()
+        _lib.check(L.tmfwm_lapack_svd_blocks(D.data_ptr(), n, b, U.data_ptr() if want_vectors else None, S.data_ptr(),
+                                             Vt.data_ptr() if want_vectors else None, int(want_vectors), _lib.MEM_DEVICE,
+                                             _stream(None)), "lapack_svd_blocks")
+    return U, S, Vt
 
 
 def prepare_tile(watermark_l: torch.Tensor, tile_height: int, tile_width: int, preserve_ratio: bool = False,

@@ -230,6 +230,31 @@ __global__ __launch_bounds__(64, kEmbedWaves<B>) void embed_kernel(EmbedArgs a)
             Vf[r][k] = (float)V[r][k];
         }
     }
+    // Conditioning test (oracle orc_svd_flag): a block whose factors could
+    // round differently from LAPACK's goes to the dgesdd route (embed_fixup_kernel).
+    // m = min over triplets reaching the output (f32(sigma_k) != 0) of min(sigma_k,
+    // distance to the nearest other sigma); flagged iff m * 2^20 < sigma_1.
+    {
+        double g[B], s1 = 0.0;
+#pragma unroll
+        for (int k = 0; k < B; ++k) {
+            g[k] = sig[k];
+            s1 = sig[k] > s1 ? sig[k] : s1;
+        }
+#pragma unroll
+        for (int k = 0; k < B; ++k)
+#pragma unroll
+            for (int j = k + 1; j < B; ++j) {
+                const double d = __builtin_fabs(sig[k] - sig[j]);
+                g[k] = d < g[k] ? d : g[k];
+                g[j] = d < g[j] ? d : g[j];
+            }
+        double m = s1;
+#pragma unroll
+        for (int k = 0; k < B; ++k) m = ((float)sig[k] != 0.0f && g[k] < m) ? g[k] : m;
+        if (m * 1048576.0 < s1 && pos.valid && q == 0)
+            a.fb_list[atomicAdd(a.fb_count, 1u)] = (uint32_t)(((int64_t)blockIdx.y * a.nbh + pos.bi) * a.nbw + pos.bj);
+    }
     bool zero = true;
 #pragma unroll
     for (int k = 0; k < B; ++k) zero = zero && (sig[k] == 0.0);

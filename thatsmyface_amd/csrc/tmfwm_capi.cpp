@@ -5,7 +5,9 @@
 
 #include <cmath>
 #include <cstdarg>
+#include <cstdint>
 #include <cstdio>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -103,7 +105,127 @@ bool ranges_overlap(const void *a, size_t na, const void *b, size_t nb)
 
 size_t span_bytes(int64_t n, int64_t stride, int64_t frame_bytes) { return n == 0 ? 0 : (size_t)((n - 1) * stride + frame_bytes); }
 
+// The per-call workspaces below come from the device's stream-ordered pool; keep freed
+// memory in the pool instead of returning it at every synchronisation (once per device).
+void keep_pool_memory(hipStream_t st)
+{
+    static std::mutex mu;
+    static std::vector<int> done;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) { (void)hipGetLastError(); return; }
+    (void)st;
+    std::lock_guard<std::mutex> lk(mu);
+    for (int d : done)
+        if (d == dev) return;
+    hipMemPool_t pool;
+    if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
+        uint64_t keep = UINT64_MAX;
+        (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+    }
+    (void)hipGetLastError();
+    done.push_back(dev);
+}
+
+// Second-pass bookkeeping: frames go in chunks of at most kListCap
+// blocks (and 65535 frames, the grid's y limit); each chunk's first pass appends the
+// blocks that need the dgesdd route to one shared id list (u32, chunk-relative) and
+// counts them in its own slot of `counts`; its fixup pass runs right after it on the
+// same stream.  kListCap = 2^26 ids = 256 MB: 517 4K frames at b = 8 per chunk.
+constexpr int64_t kListCap = int64_t(1) << 26;
+
+struct Chunks {
+    int64_t per_frame = 0, frames = 0, n = 0, cap = 0;
+    void plan(int64_t nframes, int64_t blocks_per_frame)
+    {
+        per_frame = blocks_per_frame;
+        frames = blocks_per_frame > 0 ? kListCap / blocks_per_frame : nframes;
+        if (frames < 1) frames = 1;
+        if (frames > 65535) frames = 65535;
+        if (frames > nframes) frames = nframes;
+        n = frames > 0 ? (nframes + frames - 1) / frames : 0;
+        cap = frames * blocks_per_frame;
+    }
+};
+
+// copy the per-chunk counts back (synchronises the stream) and sum them
+int sum_counts(const uint32_t *dcounts, int64_t nchunks, hipStream_t st, int64_t *out)
+{
+    std::vector<uint32_t> h((size_t)nchunks);
+    if (nchunks) {
+        hipError_t e = hipMemcpyAsync(h.data(), dcounts, (size_t)nchunks * 4, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) return fail(TMFWM_ERR_HIP, "reading the dgesdd-route counts failed: %s", hipGetErrorString(e));
+    }
+    int64_t t = 0;
+    for (uint32_t v : h) t += v;
+    *out = t;
+    return 0;
+}
+
 }  // namespace
+
+namespace tmf {
+// Both passes of embed over device-resident frames (a.src / a.dst / a.wm set).
+int run_embed(EmbedArgs a, hipStream_t st, int64_t *n_lapack)
+{
+    Chunks ch;
+    ch.plan(a.nframes, (int64_t)a.nbh * a.nbw);
+    DevBuf list, counts;
+    if (ch.cap > 0) {
+        keep_pool_memory(st);
+        if (int rc = list.alloc((size_t)ch.cap * 4, st, "dgesdd-route block list")) return rc;
+        if (int rc = counts.alloc((size_t)ch.n * 4, st, "dgesdd-route counts")) return rc;
+        TMF_HIP(hipMemsetAsync(counts.p, 0, (size_t)ch.n * 4, st));
+    }
+    if (ch.cap == 0) {  // no full block: colour round trip only
+        TMF_HIP(launch_embed(a, st));
+        if (n_lapack) *n_lapack = 0;
+        return 0;
+    }
+    for (int64_t c = 0; c < ch.n; ++c) {
+        EmbedArgs k = a;
+        const int64_t f0 = c * ch.frames;
+        k.nframes = a.nframes - f0 < ch.frames ? a.nframes - f0 : ch.frames;
+        k.src = a.src + f0 * a.frame_stride;
+        k.dst = a.dst + f0 * a.frame_stride;
+        k.fb_list = static_cast<uint32_t *>(list.p);
+        k.fb_count = static_cast<uint32_t *>(counts.p) + c;
+        TMF_HIP(launch_embed(k, st));
+        TMF_HIP(launch_embed_fixup(k, k.fb_list, k.fb_count, k.nframes * ch.per_frame, st));
+    }
+    if (n_lapack) return sum_counts(static_cast<const uint32_t *>(counts.p), ch.n, st, n_lapack);
+    return 0;
+}
+
+int run_extract(ExtractArgs a, hipStream_t st, int64_t *n_lapack)
+{
+    Chunks ch;
+    ch.plan(a.nframes, (int64_t)a.nbh * a.nbw);
+    if (ch.cap == 0) {
+        if (n_lapack) *n_lapack = 0;
+        return 0;
+    }
+    keep_pool_memory(st);
+    DevBuf list, counts;
+    if (int rc = list.alloc((size_t)ch.cap * 4, st, "dgesdd-route block list")) return rc;
+    if (int rc = counts.alloc((size_t)ch.n * 4, st, "dgesdd-route counts")) return rc;
+    TMF_HIP(hipMemsetAsync(counts.p, 0, (size_t)ch.n * 4, st));
+    for (int64_t c = 0; c < ch.n; ++c) {
+        ExtractArgs k = a;
+        const int64_t f0 = c * ch.frames;
+        k.nframes = a.nframes - f0 < ch.frames ? a.nframes - f0 : ch.frames;
+        k.wsrc = a.wsrc + f0 * a.frame_stride;
+        k.osrc = a.osrc + f0 * a.frame_stride;
+        k.out = a.out + f0 * a.tile_stride;
+        k.fb_list = static_cast<uint32_t *>(list.p);
+        k.fb_count = static_cast<uint32_t *>(counts.p) + c;
+        TMF_HIP(launch_extract(k, st));
+        TMF_HIP(launch_extract_fixup(k, k.fb_list, k.fb_count, k.nframes * ch.per_frame, st));
+    }
+    if (n_lapack) return sum_counts(static_cast<const uint32_t *>(counts.p), ch.n, st, n_lapack);
+    return 0;
+}
+}  // namespace tmf
 
 extern "C" {
 
@@ -121,10 +243,12 @@ int tmfwm_device_count(void)
     return n;
 }
 
-int tmfwm_embed(const uint8_t *rgb, int64_t n_frames, int32_t height, int32_t width, int64_t frame_stride,
-                const uint8_t *wm_tile, int32_t block, double alpha, uint8_t *out, int32_t mem_kind, void *hip_stream)
+int tmfwm_embed_ex(const uint8_t *rgb, int64_t n_frames, int32_t height, int32_t width, int64_t frame_stride,
+                   const uint8_t *wm_tile, int32_t block, double alpha, uint8_t *out, int32_t mem_kind, void *hip_stream,
+                   int64_t *n_lapack_blocks)
 {
     t_err.clear();
+    if (n_lapack_blocks) *n_lapack_blocks = 0;
     if (int rc = check_frames(n_frames, height, width, frame_stride, block)) return rc;
     if (!std::isfinite(alpha)) return fail(TMFWM_ERR_INVALID, "alpha is not finite");
     if (int rc = need_device()) return rc;
@@ -154,8 +278,7 @@ int tmfwm_embed(const uint8_t *rgb, int64_t n_frames, int32_t height, int32_t wi
         a.dst = out;
         a.wm = wm_tile;
         a.aligned = ((reinterpret_cast<uintptr_t>(rgb) | reinterpret_cast<uintptr_t>(out)) % 4 == 0) && frame_stride % 4 == 0 && width % 4 == 0;
-        TMF_HIP(tmf::launch_embed(a, st));
-        return 0;
+        return tmf::run_embed(a, st, n_lapack_blocks);
     }
     if (mem_kind != TMFWM_MEM_HOST) return fail(TMFWM_ERR_INVALID, "mem_kind %d", mem_kind);
     if (!rgb || !out || (tbytes && !wm_tile)) return fail(TMFWM_ERR_INVALID, "NULL host pointer");
@@ -169,7 +292,7 @@ int tmfwm_embed(const uint8_t *rgb, int64_t n_frames, int32_t height, int32_t wi
     a.dst = static_cast<uint8_t *>(dout.p);
     a.wm = static_cast<const uint8_t *>(dwm.p);
     a.aligned = frame_stride % 4 == 0 && width % 4 == 0;
-    TMF_HIP(tmf::launch_embed(a, st));
+    if (int rc = tmf::run_embed(a, st, n_lapack_blocks)) return rc;
     if (frame_stride == fbytes) {
         TMF_HIP(hipMemcpyAsync(out, dout.p, span, hipMemcpyDeviceToHost, st));
     } else {
@@ -181,10 +304,18 @@ int tmfwm_embed(const uint8_t *rgb, int64_t n_frames, int32_t height, int32_t wi
     return 0;
 }
 
-int tmfwm_extract(const uint8_t *wm_rgb, const uint8_t *orig_rgb, int64_t n_frames, int32_t height, int32_t width,
-                  int64_t frame_stride, int32_t block, double alpha, uint8_t *out_tiles, int32_t mem_kind, void *hip_stream)
+int tmfwm_embed(const uint8_t *rgb, int64_t n_frames, int32_t height, int32_t width, int64_t frame_stride,
+                const uint8_t *wm_tile, int32_t block, double alpha, uint8_t *out, int32_t mem_kind, void *hip_stream)
+{
+    return tmfwm_embed_ex(rgb, n_frames, height, width, frame_stride, wm_tile, block, alpha, out, mem_kind, hip_stream, nullptr);
+}
+
+int tmfwm_extract_ex(const uint8_t *wm_rgb, const uint8_t *orig_rgb, int64_t n_frames, int32_t height, int32_t width,
+                     int64_t frame_stride, int32_t block, double alpha, uint8_t *out_tiles, int32_t mem_kind, void *hip_stream,
+                     int64_t *n_lapack_blocks)
 {
     t_err.clear();
+    if (n_lapack_blocks) *n_lapack_blocks = 0;
     if (int rc = check_frames(n_frames, height, width, frame_stride, block)) return rc;
     if (!std::isfinite(alpha) || alpha == 0.0) return fail(TMFWM_ERR_INVALID, "alpha must be finite and non-zero");
     if (int rc = need_device()) return rc;
@@ -215,8 +346,7 @@ int tmfwm_extract(const uint8_t *wm_rgb, const uint8_t *orig_rgb, int64_t n_fram
         a.osrc = orig_rgb;
         a.out = out_tiles;
         a.aligned = ((reinterpret_cast<uintptr_t>(wm_rgb) | reinterpret_cast<uintptr_t>(orig_rgb)) % 4 == 0) && frame_stride % 4 == 0 && width % 4 == 0;
-        TMF_HIP(tmf::launch_extract(a, st));
-        return 0;
+        return tmf::run_extract(a, st, n_lapack_blocks);
     }
     if (mem_kind != TMFWM_MEM_HOST) return fail(TMFWM_ERR_INVALID, "mem_kind %d", mem_kind);
     if (!wm_rgb || !orig_rgb || !out_tiles) return fail(TMFWM_ERR_INVALID, "NULL host pointer");
@@ -230,10 +360,17 @@ int tmfwm_extract(const uint8_t *wm_rgb, const uint8_t *orig_rgb, int64_t n_fram
     a.osrc = static_cast<const uint8_t *>(dor.p);
     a.out = static_cast<uint8_t *>(dout.p);
     a.aligned = frame_stride % 4 == 0 && width % 4 == 0;
-    TMF_HIP(tmf::launch_extract(a, st));
+    if (int rc = tmf::run_extract(a, st, n_lapack_blocks)) return rc;
     TMF_HIP(hipMemcpyAsync(out_tiles, dout.p, (size_t)(tbytes * n_frames), hipMemcpyDeviceToHost, st));
     TMF_HIP(hipStreamSynchronize(st));
     return 0;
+}
+
+int tmfwm_extract(const uint8_t *wm_rgb, const uint8_t *orig_rgb, int64_t n_frames, int32_t height, int32_t width,
+                  int64_t frame_stride, int32_t block, double alpha, uint8_t *out_tiles, int32_t mem_kind, void *hip_stream)
+{
+    return tmfwm_extract_ex(wm_rgb, orig_rgb, n_frames, height, width, frame_stride, block, alpha, out_tiles, mem_kind,
+                            hip_stream, nullptr);
 }
 
 int tmfwm_rgb_to_ycbcr(const uint8_t *rgb, int64_t npix, float *ycc, int32_t mem_kind, void *hip_stream)
@@ -341,6 +478,86 @@ int tmfwm_svd_blocks(const float *D, int64_t n_blocks, int32_t block, float *U, 
     TMF_HIP(hipMemcpyAsync(S, dS.p, sb, hipMemcpyDeviceToHost, st));
     TMF_HIP(hipMemcpyAsync(Vt, dV.p, mb, hipMemcpyDeviceToHost, st));
     if (sweeps) TMF_HIP(hipMemcpyAsync(sweeps, dW.p, (size_t)n_blocks * 4, hipMemcpyDeviceToHost, st));
+    TMF_HIP(hipStreamSynchronize(st));
+    return 0;
+}
+
+int tmfwm_lapack_svd_blocks(const float *D, int64_t n_blocks, int32_t block, float *U, float *S, float *Vt, int32_t want_vectors,
+                            int32_t mem_kind, void *hip_stream)
+{
+    t_err.clear();
+    if (n_blocks < 0) return fail(TMFWM_ERR_INVALID, "n_blocks < 0");
+    if (int rc = check_frames(0, 0, 0, 0, block)) return rc;
+    if (int rc = need_device()) return rc;
+    if (n_blocks == 0) return 0;
+    hipStream_t st = pick_stream(hip_stream);
+    const size_t mb = (size_t)n_blocks * block * block * sizeof(float), sb = (size_t)n_blocks * block * sizeof(float);
+    DevBuf dinfo;
+    if (int rc = dinfo.alloc((size_t)n_blocks * 4, st, "info")) return rc;
+    int32_t *info = static_cast<int32_t *>(dinfo.p);
+    const float *dD = D;
+    float *dU = U, *dS = S, *dVt = Vt;
+    DevBuf bD, bU, bS, bV;
+    if (mem_kind == TMFWM_MEM_DEVICE) {
+        if (int rc = check_device_ptr(D, "D")) return rc;
+        if (int rc = check_device_ptr(S, "S")) return rc;
+        if (want_vectors) {
+            if (int rc = check_device_ptr(U, "U")) return rc;
+            if (int rc = check_device_ptr(Vt, "Vt")) return rc;
+        }
+    } else {
+        if (mem_kind != TMFWM_MEM_HOST || !D || !S || (want_vectors && (!U || !Vt))) return fail(TMFWM_ERR_INVALID, "bad host arguments");
+        if (int rc = bD.alloc(mb, st, "D")) return rc;
+        if (int rc = bS.alloc(sb, st, "S")) return rc;
+        if (want_vectors) {
+            if (int rc = bU.alloc(mb, st, "U")) return rc;
+            if (int rc = bV.alloc(mb, st, "Vt")) return rc;
+        }
+        TMF_HIP(hipMemcpyAsync(bD.p, D, mb, hipMemcpyHostToDevice, st));
+        dD = static_cast<const float *>(bD.p);
+        dS = static_cast<float *>(bS.p);
+        dU = static_cast<float *>(bU.p);
+        dVt = static_cast<float *>(bV.p);
+    }
+    TMF_HIP(tmf::launch_lapack_svd_blocks(dD, n_blocks, block, dU, dS, dVt, want_vectors != 0, info, st));
+    if (mem_kind == TMFWM_MEM_HOST) {
+        TMF_HIP(hipMemcpyAsync(S, dS, sb, hipMemcpyDeviceToHost, st));
+        if (want_vectors) {
+            TMF_HIP(hipMemcpyAsync(U, dU, mb, hipMemcpyDeviceToHost, st));
+            TMF_HIP(hipMemcpyAsync(Vt, dVt, mb, hipMemcpyDeviceToHost, st));
+        }
+    }
+    // dbdsqr's convergence flag of every block (LAPACK's info > 0): reported, never silent
+    std::vector<int32_t> h((size_t)n_blocks);
+    TMF_HIP(hipMemcpyAsync(h.data(), info, (size_t)n_blocks * 4, hipMemcpyDeviceToHost, st));
+    TMF_HIP(hipStreamSynchronize(st));
+    for (int64_t k = 0; k < n_blocks; ++k)
+        if (h[(size_t)k]) return fail(TMFWM_ERR_INVALID, "dbdsqr did not converge on block %lld", (long long)k);
+    return 0;
+}
+
+int tmfwm_lapack_nrm2(const double *x, int64_t n_vectors, int32_t n, int32_t inc, double *out, int32_t mem_kind, void *hip_stream)
+{
+    t_err.clear();
+    if (n_vectors < 0 || n < 0 || inc < 1) return fail(TMFWM_ERR_INVALID, "bad sizes");
+    if (int rc = need_device()) return rc;
+    if (n_vectors == 0) return 0;
+    hipStream_t st = pick_stream(hip_stream);
+    const size_t xb = (size_t)n_vectors * n * inc * sizeof(double), ob = (size_t)n_vectors * sizeof(double);
+    if (mem_kind == TMFWM_MEM_DEVICE) {
+        if (xb)
+            if (int rc = check_device_ptr(x, "x")) return rc;
+        if (int rc = check_device_ptr(out, "out")) return rc;
+        TMF_HIP(tmf::launch_lapack_nrm2(x, n_vectors, n, inc, out, st));
+        return 0;
+    }
+    if (mem_kind != TMFWM_MEM_HOST || !out || (xb && !x)) return fail(TMFWM_ERR_INVALID, "bad host arguments");
+    DevBuf dx, dout;
+    if (int rc = dx.alloc(xb, st, "x")) return rc;
+    if (int rc = dout.alloc(ob, st, "out")) return rc;
+    if (xb) TMF_HIP(hipMemcpyAsync(dx.p, x, xb, hipMemcpyHostToDevice, st));
+    TMF_HIP(tmf::launch_lapack_nrm2(static_cast<const double *>(dx.p), n_vectors, n, inc, static_cast<double *>(dout.p), st));
+    TMF_HIP(hipMemcpyAsync(out, dout.p, ob, hipMemcpyDeviceToHost, st));
     TMF_HIP(hipStreamSynchronize(st));
     return 0;
 }

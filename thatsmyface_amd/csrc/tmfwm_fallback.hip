@@ -1,0 +1,212 @@
+// The dgesdd route on the GPU (tmfwm_lapack.h): the second pass of embed and extract,
+// plus the stage entry points the parity tests call.
+//
+// embed_kernel<b> runs the Jacobi route on every block and appends to a list the blocks
+// whose conditioning test fails; embed_fixup_kernel<b> redoes exactly
+// those blocks end to end -- luma, DCT, np.linalg.svd as LAPACK computes it, blend,
+// reconstruct, IDCT, inverse colour -- and overwrites their pixels.  extract_kernel<b>
+// appends the blocks whose sigma_1 enclosure does not decide f32(sigma_1) for either
+// image; extract_fixup_kernel<b> computes both sigma_1 on the dgesdd route and writes the
+// byte.  One thread per listed block; a grid-stride loop over the device-side count,
+// so no host round trip sits between the passes.
+#include "tmfwm_device.h"
+#include "tmfwm_internal.h"
+#include "tmfwm_lapack.h"
+
+namespace tmf {
+
+template <int B>
+TMF_DEVI void load_dct_block(const uint8_t *frame, int W, int bi, int bj, float (&y)[B][B])
+{
+#pragma unroll
+    for (int r = 0; r < B; ++r)
+#pragma unroll
+        for (int c = 0; c < B; ++c) {
+            const uint8_t *p = frame + ((int64_t)(bi * B + r) * W + (int64_t)bj * B + c) * 3;
+            y[r][c] = luma(p[0], p[1], p[2]);
+        }
+    // :192 / :279-282 -- DCT along axis 0, then axis 1
+#pragma unroll
+    for (int c = 0; c < B; ++c) {
+        float col[B];
+#pragma unroll
+        for (int r = 0; r < B; ++r) col[r] = y[r][c];
+        dct::dct2<B>(col);
+#pragma unroll
+        for (int r = 0; r < B; ++r) y[r][c] = col[r];
+    }
+#pragma unroll
+    for (int r = 0; r < B; ++r) dct::dct2<B>(y[r]);
+}
+
+template <int B>
+__global__ __launch_bounds__(64) void embed_fixup_kernel(EmbedArgs a, const uint32_t *__restrict__ list, const uint32_t *__restrict__ count)
+{
+    const uint32_t n = *count;
+    const uint32_t per_frame = (uint32_t)a.nbh * (uint32_t)a.nbw;
+    for (uint32_t t = blockIdx.x * 64u + threadIdx.x; t < n; t += gridDim.x * 64u) {
+        const uint32_t id = list[t];
+        const int64_t f = id / per_frame;
+        const uint32_t rem = id % per_frame;
+        const int bi = (int)(rem / (uint32_t)a.nbw), bj = (int)(rem % (uint32_t)a.nbw);
+        const uint8_t *src = a.src + f * a.frame_stride;
+        uint8_t *dst = a.dst + f * a.frame_stride;
+        float x[B][B];
+        load_dct_block<B>(src, a.W, bi, bj, x);
+        float U[B * B], S[B], Vt[B * B];
+        lp::svd_f32<true>(&x[0][0], B, U, S, Vt);  // :195
+        // :198 blend, :201 U @ (diag(S) @ Vt) as OpenBLAS sgemm's fma chain over k
+        const double w = (double)a.wm[(int64_t)bi * a.nbw + bj];
+        S[0] = (float)((double)S[0] + a.alpha * (w / 255.0));
+#pragma unroll
+        for (int i = 0; i < B; ++i)
+#pragma unroll
+            for (int j = 0; j < B; ++j) {
+                float acc = 0.0f;
+#pragma unroll
+                for (int k = 0; k < B; ++k) acc = __builtin_fmaf(U[i * B + k], S[k] * Vt[k * B + j], acc);
+                x[i][j] = acc;
+            }
+        // :204 IDCT, axis 0 then axis 1
+#pragma unroll
+        for (int c = 0; c < B; ++c) {
+            float col[B];
+#pragma unroll
+            for (int r = 0; r < B; ++r) col[r] = x[r][c];
+            dct::dct3<B>(col);
+#pragma unroll
+            for (int r = 0; r < B; ++r) x[r][c] = col[r];
+        }
+#pragma unroll
+        for (int r = 0; r < B; ++r) dct::dct3<B>(x[r]);
+        // :207-216 write back with the pixel's own chroma, inverse colour
+#pragma unroll
+        for (int r = 0; r < B; ++r)
+#pragma unroll
+            for (int c = 0; c < B; ++c) {
+                const int64_t off = ((int64_t)(bi * B + r) * a.W + (int64_t)bj * B + c) * 3;
+                float cbs, crs;
+                chroma(src[off], src[off + 1], src[off + 2], cbs, crs);
+                uint32_t R8, G8, B8;
+                colour_inv(x[r][c], cbs, crs, R8, G8, B8);
+                dst[off] = (uint8_t)R8;
+                dst[off + 1] = (uint8_t)G8;
+                dst[off + 2] = (uint8_t)B8;
+            }
+    }
+}
+
+template <int B>
+__global__ __launch_bounds__(64) void extract_fixup_kernel(ExtractArgs a, const uint32_t *__restrict__ list, const uint32_t *__restrict__ count)
+{
+    const uint32_t n = *count;
+    const uint32_t per_frame = (uint32_t)a.nbh * (uint32_t)a.nbw;
+    for (uint32_t t = blockIdx.x * 64u + threadIdx.x; t < n; t += gridDim.x * 64u) {
+        const uint32_t id = list[t];
+        const int64_t f = id / per_frame;
+        const uint32_t rem = id % per_frame;
+        const int bi = (int)(rem / (uint32_t)a.nbw), bj = (int)(rem % (uint32_t)a.nbw);
+        float sig[2];
+        for (int img = 0; img < 2; ++img) {
+            float x[B][B];
+            load_dct_block<B>((img == 0 ? a.wsrc : a.osrc) + f * a.frame_stride, a.W, bi, bj, x);
+            float S[B];
+            lp::svd_f32<false>(&x[0][0], B, nullptr, S, nullptr);  // :279-282, S only
+            sig[img] = S[0];
+        }
+        // :285-289 (numpy-2 NEP 50): f32 difference / f32(alpha); clip and *255 in f64; truncate
+        const float e = (sig[0] - sig[1]) / a.alpha32;
+        double d = (double)e;
+        d = d < 0.0 ? 0.0 : d;
+        d = d > 1.0 ? 1.0 : d;
+        a.out[f * a.tile_stride + (int64_t)bi * a.nbw + bj] = (uint8_t)(uint32_t)(d * 255.0);
+    }
+}
+
+// stage entry points (tmfwm_lapack_svd_blocks, tmfwm_lapack_nrm2)
+__global__ __launch_bounds__(64) void lp_svd_blocks_kernel(const float *__restrict__ D, int64_t nb, int b, float *__restrict__ U,
+                                                           float *__restrict__ S, float *__restrict__ Vt, int want_v,
+                                                           int32_t *__restrict__ info)
+{
+    const int64_t k = (int64_t)blockIdx.x * 64 + threadIdx.x;
+    if (k >= nb) return;
+    const int64_t o = k * b * b;
+    const int rc = want_v ? lp::svd_f32<true>(D + o, b, U + o, S + k * b, Vt + o)
+                          : lp::svd_f32<false>(D + o, b, nullptr, S + k * b, nullptr);
+    if (info) info[k] = rc;
+}
+
+__global__ __launch_bounds__(64) void lp_nrm2_kernel(const double *__restrict__ x, int64_t nvec, int n, int inc, double *__restrict__ out)
+{
+    const int64_t k = (int64_t)blockIdx.x * 64 + threadIdx.x;
+    if (k < nvec) out[k] = lp::dnrm2(n, x + k * (int64_t)n * inc, inc);
+}
+
+// ---------------------------------------------------------------------------
+// launchers: the fixup grid is sized for the worst case (every block listed) but
+// capped; threads beyond the device-side count exit at once
+// ---------------------------------------------------------------------------
+static unsigned fixup_grid(int64_t max_entries)
+{
+    const int64_t g = (max_entries + 63) / 64;
+    return (unsigned)(g < 1 ? 1 : (g > 4096 ? 4096 : g));
+}
+
+template <int B>
+static void embed_fixup_b(const EmbedArgs &a, const uint32_t *list, const uint32_t *count, int64_t max_entries, hipStream_t st)
+{
+    hipLaunchKernelGGL(embed_fixup_kernel<B>, dim3(fixup_grid(max_entries)), dim3(64), 0, st, a, list, count);
+}
+
+hipError_t launch_embed_fixup(const EmbedArgs &a, const uint32_t *list, const uint32_t *count, int64_t max_entries, hipStream_t st)
+{
+    switch (a.block) {
+    case 4: embed_fixup_b<4>(a, list, count, max_entries, st); break;
+    case 6: embed_fixup_b<6>(a, list, count, max_entries, st); break;
+    case 8: embed_fixup_b<8>(a, list, count, max_entries, st); break;
+    case 10: embed_fixup_b<10>(a, list, count, max_entries, st); break;
+    case 12: embed_fixup_b<12>(a, list, count, max_entries, st); break;
+    case 14: embed_fixup_b<14>(a, list, count, max_entries, st); break;
+    case 16: embed_fixup_b<16>(a, list, count, max_entries, st); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+template <int B>
+static void extract_fixup_b(const ExtractArgs &a, const uint32_t *list, const uint32_t *count, int64_t max_entries, hipStream_t st)
+{
+    hipLaunchKernelGGL(extract_fixup_kernel<B>, dim3(fixup_grid(max_entries)), dim3(64), 0, st, a, list, count);
+}
+
+hipError_t launch_extract_fixup(const ExtractArgs &a, const uint32_t *list, const uint32_t *count, int64_t max_entries, hipStream_t st)
+{
+    switch (a.block) {
+    case 4: extract_fixup_b<4>(a, list, count, max_entries, st); break;
+    case 6: extract_fixup_b<6>(a, list, count, max_entries, st); break;
+    case 8: extract_fixup_b<8>(a, list, count, max_entries, st); break;
+    case 10: extract_fixup_b<10>(a, list, count, max_entries, st); break;
+    case 12: extract_fixup_b<12>(a, list, count, max_entries, st); break;
+    case 14: extract_fixup_b<14>(a, list, count, max_entries, st); break;
+    case 16: extract_fixup_b<16>(a, list, count, max_entries, st); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_lapack_svd_blocks(const float *D, int64_t nb, int block, float *U, float *S, float *Vt, int want_v, int32_t *info,
+                                    hipStream_t st)
+{
+    if (nb == 0) return hipSuccess;
+    hipLaunchKernelGGL(lp_svd_blocks_kernel, dim3((unsigned)((nb + 63) / 64)), dim3(64), 0, st, D, nb, block, U, S, Vt, want_v, info);
+    return hipGetLastError();
+}
+
+hipError_t launch_lapack_nrm2(const double *x, int64_t nvec, int n, int inc, double *out, hipStream_t st)
+{
+    if (nvec == 0) return hipSuccess;
+    hipLaunchKernelGGL(lp_nrm2_kernel, dim3((unsigned)((nvec + 63) / 64)), dim3(64), 0, st, x, nvec, n, inc, out);
+    return hipGetLastError();
+}
+
+}  // namespace tmf

@@ -16,6 +16,10 @@ struct EmbedArgs {
     int H, W, block, nbh, nbw, strips_per_row;
     int aligned;             // 4-byte aligned pixel rows: dword loads/stores
     double alpha;
+    // blocks the conditioning test sends to the dgesdd route: ids (frame * nbh + bi) * nbw + bj
+    // relative to this launch, appended at fb_list[atomicAdd(fb_count, 1)]
+    uint32_t *fb_list;
+    uint32_t *fb_count;
 };
 
 struct ExtractArgs {
@@ -28,6 +32,8 @@ struct ExtractArgs {
     int H, W, block, nbh, nbw, strips_per_row;
     int aligned;
     float alpha32;           // f32(alpha): numpy-2 weak-scalar promotion (watermarking.py:285)
+    uint32_t *fb_list;       // blocks whose sigma_1 enclosure is undecided (dgesdd route)
+    uint32_t *fb_count;
 };
 
 struct EdgeArgs {
@@ -43,6 +49,12 @@ hipError_t launch_extract(const ExtractArgs &a, hipStream_t st);
 hipError_t launch_rgb_to_ycbcr(const uint8_t *rgb, int64_t npix, float *ycc, hipStream_t st);
 hipError_t launch_ycbcr_to_rgb(const float *ycc, int64_t npix, uint8_t *rgb, hipStream_t st);
 hipError_t launch_dct2d_blocks(float *blocks, int64_t nb, int block, int inverse, hipStream_t st);
+// second pass on the dgesdd route (tmfwm_fallback.hip); max_entries bounds the list
+hipError_t launch_embed_fixup(const EmbedArgs &a, const uint32_t *list, const uint32_t *count, int64_t max_entries, hipStream_t st);
+hipError_t launch_extract_fixup(const ExtractArgs &a, const uint32_t *list, const uint32_t *count, int64_t max_entries, hipStream_t st);
+hipError_t launch_lapack_svd_blocks(const float *D, int64_t nb, int block, float *U, float *S, float *Vt, int want_v, int32_t *info,
+                                    hipStream_t st);
+hipError_t launch_lapack_nrm2(const double *x, int64_t nvec, int n, int inc, double *out, hipStream_t st);
 hipError_t launch_svd_blocks(const float *D, int64_t nb, int block, float *U, float *S, float *Vt, int32_t *sweeps, hipStream_t st);
 // Watermark-tile preparation (tmfwm_tile.hip): Pillow's LANCZOS resample tables.
 struct ResampleAxis {

@@ -27,32 +27,13 @@ extern template __global__ void embed_kernel<8>(EmbedArgs);  // tmfwm_embed8.hip
 constexpr int kPowerIters = TMF_POWER_ITERS;  // f32 power iterations before certification
 
 template <int B>
-TMF_DEVI float sigma1_of(const uint32_t (&words)[Geo<B>::R][Geo<B>::NW], int q, float *tile)
+TMF_DEVI bool sigma1_of(const uint32_t (&words)[Geo<B>::R][Geo<B>::NW], int q, float *tile, float &s1)
 {
     constexpr int L = Geo<B>::L, R = Geo<B>::R;
     float x[R][B];
     luma_rows<B>(words, x);
     dct2d_rows_layout<B, false>(x, tile, q);
-    float s1;
-    const bool ok = sigma1_certified<B, L, kPowerIters>(x, s1);
-    if (!__all(ok)) {
-        // exact path (the oracle's Jacobi) for the blocks the enclosure could not decide;
-        // certified blocks enter as zero matrices and leave the sweeps at once
-        double A[R][B], V[R][B];
-#pragma unroll
-        for (int r = 0; r < R; ++r)
-#pragma unroll
-            for (int c = 0; c < B; ++c) A[r][c] = ok ? 0.0 : (double)x[r][c];
-        jacobi<double, B, L, false>(A, V, q);
-        double m = 0.0;
-#pragma unroll
-        for (int k = 0; k < B; ++k) {
-            const double s = __builtin_sqrt(cdot<R, B, L>(A, k, k));
-            m = s > m ? s : m;
-        }
-        if (!ok) s1 = (float)m;
-    }
-    return s1;
+    return sigma1_certified<B, L, kPowerIters>(x, s1);
 }
 
 template <int B>
@@ -65,27 +46,33 @@ __global__ __launch_bounds__(64, (B > 8 ? 2 : 3)) void extract_kernel(ExtractArg
     const StripPos pos = strip_pos<B>(a.strips_per_row, a.nbw);
     // b <= 12: both images' rows are requested up front -- one exposed HBM latency per
     // wave, not two (~4 % at b = 8, and only at 3 waves/SIMD, hence the launch bound).
-    // b >= 14: the extra live rows would push the fallback Jacobi into spills.
     float sw, so;
+    bool ok;
     if constexpr (B <= 12) {
         uint32_t ww[Geo<B>::R][Geo<B>::NW], wo[Geo<B>::R][Geo<B>::NW];
         load_block_rows<B>(a.wsrc + pos.frame * a.frame_stride, a.W, pos, q, a.aligned, ww);
         load_block_rows<B>(a.osrc + pos.frame * a.frame_stride, a.W, pos, q, a.aligned, wo);
-        sw = sigma1_of<B>(ww, q, tile);
-        so = sigma1_of<B>(wo, q, tile);
+        ok = sigma1_of<B>(ww, q, tile, sw);
+        ok = sigma1_of<B>(wo, q, tile, so) && ok;
     } else {
         uint32_t w[Geo<B>::R][Geo<B>::NW];
         load_block_rows<B>(a.wsrc + pos.frame * a.frame_stride, a.W, pos, q, a.aligned, w);
-        sw = sigma1_of<B>(w, q, tile);
+        ok = sigma1_of<B>(w, q, tile, sw);
         load_block_rows<B>(a.osrc + pos.frame * a.frame_stride, a.W, pos, q, a.aligned, w);
-        so = sigma1_of<B>(w, q, tile);
+        ok = sigma1_of<B>(w, q, tile, so) && ok;
+    }
+    if (!pos.valid || q != 0) return;
+    const uint32_t id = (uint32_t)(((int64_t)blockIdx.y * a.nbh + pos.bi) * a.nbw + pos.bj);
+    if (!ok) {  // the enclosure did not decide f32(sigma_1): dgesdd route (extract_fixup_kernel)
+        a.fb_list[atomicAdd(a.fb_count, 1u)] = id;
+        return;
     }
     // :285 under numpy-2 NEP 50: (f32 - f32) / f32(alpha) in f32; :288-289 clip, *255 in f64, trunc
     const float e = (sw - so) / a.alpha32;
     double d = (double)e;
     d = d < 0.0 ? 0.0 : d;
     d = d > 1.0 ? 1.0 : d;
-    if (pos.valid && q == 0) a.out[pos.frame * a.tile_stride + (int64_t)pos.bi * a.nbw + pos.bj] = (uint8_t)(uint32_t)(d * 255.0);
+    a.out[pos.frame * a.tile_stride + (int64_t)pos.bi * a.nbw + pos.bj] = (uint8_t)(uint32_t)(d * 255.0);
 }
 
 // ---------------------------------------------------------------------------
