@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define TMFWM_ABI_VERSION 2
+#define TMFWM_ABI_VERSION 3
 
 #define TMFWM_MEM_HOST 0
 #define TMFWM_MEM_DEVICE 1
@@ -97,6 +97,29 @@ int tmfwm_extract(const uint8_t *wm_rgb, const uint8_t *orig_rgb, int64_t n_fram
 int tmfwm_extract_ex(const uint8_t *wm_rgb, const uint8_t *orig_rgb, int64_t n_frames, int32_t height, int32_t width,
                      int64_t frame_stride, int32_t block, double alpha, uint8_t *out_tiles, int32_t mem_kind,
                      void *hip_stream, int64_t *n_lapack_blocks);
+
+/*
+ * Multi-GPU embed / extract for callers without torch.distributed (one process drives
+ * several devices).  Host memory only: rgb / out (wm_rgb / orig_rgb / out_tiles) are host
+ * buffers laid out as for tmfwm_embed / tmfwm_extract, and the call returns when every
+ * result is back.  The n_frames frames are split into n_shards contiguous shards (sizes
+ * differ by at most one, shard s gets frames [s*n/k + min(s, n%k), ...)), shard s runs on
+ * HIP device devices[s] (devices = NULL: device s; n_shards <= 0 with devices = NULL: every
+ * visible device) on its own host thread and stream, in passes of at most ~2 GiB of
+ * frames.  The watermark tile is uploaded to devices[0] and broadcast to every other
+ * device of the set with RCCL (ncclBroadcast over xGMI; librccl.so.1 is loaded on first
+ * use).  Shards naming the same device share its tile (logical shards).  Replaces the
+ * app's per-image loop (internal_pages/embed_watermark_page.py:492-558) for a batch; the
+ * per-frame arithmetic is tmfwm_embed's.  *n_lapack_blocks (optional) sums the shards'
+ * dgesdd-route blocks.  The calling thread's current HIP device is preserved.
+ */
+int tmfwm_embed_multi(const uint8_t *rgb, int64_t n_frames, int32_t height, int32_t width, int64_t frame_stride,
+                      const uint8_t *wm_tile, int32_t block, double alpha, uint8_t *out, const int32_t *devices,
+                      int32_t n_shards, int64_t *n_lapack_blocks);
+
+int tmfwm_extract_multi(const uint8_t *wm_rgb, const uint8_t *orig_rgb, int64_t n_frames, int32_t height, int32_t width,
+                        int64_t frame_stride, int32_t block, double alpha, uint8_t *out_tiles, const int32_t *devices,
+                        int32_t n_shards, int64_t *n_lapack_blocks);
 
 /* rgb_to_ycbcr (watermarking.py:23): npix RGB uint8 pixels -> npix x 3 float32 (Y, Cb+0.5, Cr+0.5). */
 int tmfwm_rgb_to_ycbcr(const uint8_t *rgb, int64_t npix, float *ycc, int32_t mem_kind, void *hip_stream);

@@ -41,6 +41,20 @@ def golden_blocks():
 
 
 @pytest.fixture(scope="session")
+def golden_alpha():
+    """Reference outputs across the app's alpha slider, up to 1.0 (gen_golden.py --alpha)."""
+    import json
+
+    import numpy as np
+
+    d = os.path.join(ROOT, "tests", "golden")
+    cases = np.load(os.path.join(d, "cases_alpha.npz"), allow_pickle=False)
+    with open(os.path.join(d, "meta_alpha.json")) as f:
+        meta = json.load(f)
+    return cases, meta
+
+
+@pytest.fixture(scope="session")
 def stages():
     import numpy as np
 

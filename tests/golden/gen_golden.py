@@ -18,6 +18,7 @@ Outputs (tests/golden/):
 
 Run:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py            (cases.npz, stages.npz, meta.json)
       PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py --blocks   (cases_blocks.npz, meta_blocks.json)
+      PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py --alpha    (cases_alpha.npz, meta_alpha.json)
 """
 from __future__ import annotations
 
@@ -144,6 +145,24 @@ BLOCK_CASES = [
 ]
 
 
+# The app's alpha slider goes to 1.0 (embed_watermark_page.py:343-350); the configs stop
+# at 0.2.  Written to cases_alpha.npz / meta_alpha.json by `gen_golden.py --alpha`.
+# Larger alpha pushes S[0] further from the cover's spectrum: more clipping in the inverse
+# colour and larger extract values (no saturation at 255 until alpha * w / 255 >= ...).
+ALPHA_CASES = [
+    (f"{kind}_{H}x{W}_b{b}_a{a}", kind, H, W, "RGB", wk, H // b, W // b, False, b, a, False)
+    for (kind, H, W, wk) in (("noise", 96, 128, "noise"), ("smooth", 112, 96, "qr"), ("qr", 128, 128, "qr"))
+    for b in (8, 16)
+    for a in (0.3, 0.5, 0.75, 1.0)
+] + [
+    ("noise_120x180_b6_a1.0", "noise", 120, 180, "RGB", "noise", 20, 30, False, 6, 1.0, False),
+    ("blocky_120x130_b12_a0.5", "blocky", 120, 130, "RGB", "noise", 10, 10, False, 12, 0.5, False),
+    ("noise_150x200_b10_a0.5_pr", "noise", 150, 200, "RGB", "qr", 21, 21, True, 10, 0.5, True),
+    ("diag_84x84_b14_a1.0", "diagonal", 84, 84, "RGB", "pattern", 6, 6, False, 14, 1.0, False),
+    ("noise_100x140_b4_a0.5", "noise", 100, 140, "RGB", "noise", 25, 35, False, 4, 0.5, False),
+]
+
+
 def _mode_img(arr: np.ndarray, mode: str):
     from PIL import Image
 
@@ -205,6 +224,23 @@ def main_blocks() -> None:
     with open(os.path.join(HERE, "meta_blocks.json"), "w") as f:
         json.dump(meta, f, indent=1, sort_keys=True)
     print("wrote cases_blocks.npz, meta_blocks.json")
+
+
+def main_alpha() -> None:
+    """cases_alpha.npz + meta_alpha.json: the app's alpha slider range up to 1.0."""
+    import PIL
+    import scipy
+
+    W = _import_reference()
+    out: dict[str, np.ndarray] = {}
+    meta: dict = {"generator": "tests/golden/gen_golden.py --alpha",
+                  "reference": "/root/reference/modules/watermarking.py (embed_watermark :135, extract_watermark :224)",
+                  "numpy": np.__version__, "scipy": scipy.__version__, "pillow": PIL.__version__, "cases": {}}
+    run_cases(W, ALPHA_CASES, 5000, out, meta)
+    np.savez_compressed(os.path.join(HERE, "cases_alpha.npz"), **out)
+    with open(os.path.join(HERE, "meta_alpha.json"), "w") as f:
+        json.dump(meta, f, indent=1, sort_keys=True)
+    print("wrote cases_alpha.npz, meta_alpha.json")
 
 
 def main() -> None:
@@ -278,5 +314,7 @@ def main() -> None:
 if __name__ == "__main__":
     if "--blocks" in sys.argv[1:]:
         main_blocks()
+    elif "--alpha" in sys.argv[1:]:
+        main_alpha()
     else:
         main()

@@ -38,7 +38,7 @@ def test_nm_exports_match_header():
 
 def test_abi_version_and_device_count():
     L = _lib.load()
-    assert L.tmfwm_abi_version() == _lib.ABI_VERSION == 2
+    assert L.tmfwm_abi_version() == _lib.ABI_VERSION == 3
     assert _lib.device_count() >= 0
 
 
@@ -82,3 +82,25 @@ def test_product_never_imports_oracle():
                 assert not re.search(r"^\s*(from|import)\s+oracle\b", src, re.M), f
                 assert "tmfwm_oracle" not in src, f
                 assert "libtmfwm_oracle" not in src, f
+
+
+def test_multi_entry_points_validate_then_need_a_device():
+    """tmfwm_embed_multi / tmfwm_extract_multi: arguments are checked first; without a GPU
+    the call fails with TMFWM_ERR_NODEVICE (no CPU fallback)."""
+    from thatsmyface_amd import multi
+
+    a = np.zeros((2, 16, 16, 3), np.uint8)
+    t = np.zeros((2, 2), np.uint8)
+    with pytest.raises(NotImplementedError):
+        multi.embed_multi(a, t, 7, 0.1)
+    with pytest.raises(ValueError):
+        multi.embed_multi(a, np.zeros((3, 3), np.uint8), 8, 0.1)
+    L = _lib.load()
+    p = lambda x: x.ctypes.data  # noqa: E731
+    with pytest.raises(ValueError):  # alpha = 0 divides by zero in extract (watermarking.py:285)
+        _lib.check(L.tmfwm_extract_multi(p(a), p(a), 2, 16, 16, 16 * 16 * 3, 8, 0.0, p(t), None, 0, None), "extract_multi")
+    if _lib.device_count() == 0:
+        with pytest.raises(_lib.TmfwmError, match="no HIP device"):
+            multi.embed_multi(a, t, 8, 0.1)
+        with pytest.raises(_lib.TmfwmError, match="no HIP device"):
+            multi.extract_multi(a, a, 8, 0.1, devices=[0, 0])

@@ -197,6 +197,21 @@ def test_golden_block_sizes_dropin_gpu(dev, golden_blocks):
         assert np.array_equal(np.asarray(ex), cases[f"{name}/extract"]), name
 
 
+def test_golden_alpha_slider_dropin_gpu(dev, golden_alpha):
+    """alpha up to 1.0 (the app's slider) through the drop-in API against the reference's bytes."""
+    from thatsmyface_amd import watermarking as W
+
+    cases, meta = golden_alpha
+    for name, m in meta["cases"].items():
+        cov = _cover_image(cases[f"{name}/cover"])
+        wm = Image.fromarray(cases[f"{name}/wm"], "L")
+        settings = {"block_size": m["block"], "alpha": m["alpha"]}
+        e = np.asarray(W.embed_watermark(cov, wm, m["preserve_ratio"], settings))
+        assert np.array_equal(e, cases[f"{name}/embed"]), name
+        ex = W.extract_watermark(Image.fromarray(cases[f"{name}/embed"]), cov, settings)
+        assert np.array_equal(np.asarray(ex), cases[f"{name}/extract"]), name
+
+
 def test_resize_watermark_golden_gpu(dev, golden, golden_blocks):
     """resize_watermark on the GPU (tmfwm_prepare_tile) gives the reference's tiles."""
     import io
@@ -294,6 +309,34 @@ def test_batch_structured_covers_vs_oracle(dev):
             assert np.array_equal(out[0].cpu().numpy(), ref), (b, kind)
             ext = batch.extract_batch(out, torch.from_numpy(c[None]).to(dev), b, 0.15)
             assert np.array_equal(ext[0].cpu().numpy(), O.extract_frame(ref, c, b, 0.15)), (b, kind)
+
+
+def test_chunked_second_pass_vs_oracle(dev, monkeypatch):
+    """Batches larger than one dgesdd-route list: with TMFWM_DEBUG_LIST_CAP at 1.5 frames'
+    worth of ids every chunk holds one frame, and each chunk's fixup pass must only touch
+    its own frames (smooth / camera-like covers flag blocks in every frame)."""
+    from golden.gen_golden import cover, wmark
+
+    from thatsmyface_amd import batch
+
+    b, H, W = 8, 272, 480
+    nb = (H // b) * (W // b)
+    host = np.stack([np.ascontiguousarray(cover(k, H, W, 30 + i)) for i, k in enumerate(("smooth", "qr", "smooth", "blocky"))])
+    t = wmark("qr", H // b, W // b, 5)
+    fr, tt = torch.from_numpy(host).to(dev), torch.from_numpy(t).to(dev)
+    st0, x0 = {}, {}
+    out0 = batch.embed_batch(fr, tt, b, 0.1, stats=st0)
+    ext0 = batch.extract_batch(out0, fr, b, 0.1, stats=x0)
+    monkeypatch.setenv("TMFWM_DEBUG_LIST_CAP", str(nb * 3 // 2))
+    st1, x1 = {}, {}
+    out1 = batch.embed_batch(fr, tt, b, 0.1, stats=st1)
+    ext1 = batch.extract_batch(out1, fr, b, 0.1, stats=x1)
+    assert st0["lapack_blocks"] > 0 and st0 == st1 and x0 == x1
+    assert torch.equal(out0, out1) and torch.equal(ext0, ext1)
+    for f in range(len(host)):
+        ref = O.embed_frame(host[f], t, b, 0.1)
+        assert np.array_equal(out1[f].cpu().numpy(), ref), f
+        assert np.array_equal(ext1[f].cpu().numpy(), O.extract_frame(ref, host[f], b, 0.1)), f
 
 
 @pytest.mark.parametrize("b", [8, 6, 12, 14])
@@ -524,3 +567,29 @@ def test_overlapping_buffers_refused(dev):
     with pytest.raises(ValueError, match="overlaps"):
         _lib.check(L.tmfwm_extract(buf.data_ptr(), buf.data_ptr(), 1, h, w, h * w * 3, b, 0.1, buf.data_ptr() + 5,
                                    _lib.MEM_DEVICE, st), "extract")
+
+
+def test_multi_entry_points_logical_shards(dev, monkeypatch):
+    """tmfwm_embed_multi / tmfwm_extract_multi (host memory, one thread + stream per shard):
+    three logical shards on device 0 == one device-resident batch == the oracle; with
+    TMFWM_DEBUG_FORCE_RCCL the tile goes through ncclCommInitAll + ncclBroadcast even on
+    one device, so the RCCL path runs on a one-GPU box."""
+    from golden.gen_golden import cover
+
+    from thatsmyface_amd import batch, multi
+
+    b, H, W, n = 8, 136, 200, 5
+    host = np.stack([np.ascontiguousarray(cover(("noise", "smooth", "qr")[i % 3], H, W, 40 + i)) for i in range(n)])
+    t = _u8(41, (H // b, W // b))
+    ref_dev = batch.embed_batch(torch.from_numpy(host).to(dev), torch.from_numpy(t).to(dev), b, 0.1).cpu().numpy()
+    for shards, force in (([0, 0, 0], "0"), ([0], "1"), ([0, 0, 0, 0, 0, 0, 0], "1")):
+        monkeypatch.setenv("TMFWM_DEBUG_FORCE_RCCL", force)
+        st, xs = {}, {}
+        out = multi.embed_multi(host, t, b, 0.1, devices=shards, stats=st)
+        assert np.array_equal(out, ref_dev), shards
+        ext = multi.extract_multi(out, host, b, 0.1, devices=shards, stats=xs)
+        for f in range(n):
+            ref = O.embed_frame(host[f], t, b, 0.1)
+            assert np.array_equal(out[f], ref), (shards, f)
+            assert np.array_equal(ext[f], O.extract_frame(ref, host[f], b, 0.1)), (shards, f)
+    assert torch.cuda.current_device() == 0

@@ -7,6 +7,7 @@
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -130,15 +131,27 @@ void keep_pool_memory(hipStream_t st)
 // blocks (and 65535 frames, the grid's y limit); each chunk's first pass appends the
 // blocks that need the dgesdd route to one shared id list (u32, chunk-relative) and
 // counts them in its own slot of `counts`; its fixup pass runs right after it on the
-// same stream.  kListCap = 2^26 ids = 256 MB: 517 4K frames at b = 8 per chunk.
-constexpr int64_t kListCap = int64_t(1) << 26;
+// same stream.  The fixup pass is latency-bound (one serial dgesdd per thread, a few ms
+// whatever the list length), so chunks are made as large as the list allows:
+// kListCap = 2^29 ids = 2 GiB (4 bytes per block, 2 % of the frames' own bytes at b = 8),
+// i.e. 4142 4K frames at b = 8 -- configs[2] / [3] take one chunk per GPU.
+// TMFWM_DEBUG_LIST_CAP (ids) lowers it so that the tests can exercise several chunks.
+constexpr int64_t kListCap = int64_t(1) << 29;
+
+int64_t list_cap()
+{
+    const char *e = std::getenv("TMFWM_DEBUG_LIST_CAP");
+    if (!e || !*e) return kListCap;
+    const long long v = std::atoll(e);
+    return v > 0 && v < kListCap ? (int64_t)v : kListCap;
+}
 
 struct Chunks {
     int64_t per_frame = 0, frames = 0, n = 0, cap = 0;
     void plan(int64_t nframes, int64_t blocks_per_frame)
     {
         per_frame = blocks_per_frame;
-        frames = blocks_per_frame > 0 ? kListCap / blocks_per_frame : nframes;
+        frames = blocks_per_frame > 0 ? list_cap() / blocks_per_frame : nframes;
         if (frames < 1) frames = 1;
         if (frames > 65535) frames = 65535;
         if (frames > nframes) frames = nframes;
@@ -165,6 +178,21 @@ int sum_counts(const uint32_t *dcounts, int64_t nchunks, hipStream_t st, int64_t
 }  // namespace
 
 namespace tmf {
+int report(int code, const char *fmt, ...)
+{
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    t_err = buf;
+    return code;
+}
+
+void clear_error() { t_err.clear(); }
+
+int check_frames(int64_t n, int32_t H, int32_t W, int64_t stride, int32_t block) { return ::check_frames(n, H, W, stride, block); }
+
 // Both passes of embed over device-resident frames (a.src / a.dst / a.wm set).
 int run_embed(EmbedArgs a, hipStream_t st, int64_t *n_lapack)
 {

@@ -43,6 +43,11 @@ struct EdgeArgs {
     int H, W, core_h, core_w, edge_w;
 };
 
+// error reporting and argument checks of the C ABI (tmfwm_capi.cpp), shared with tmfwm_multi.cpp
+int report(int code, const char *fmt, ...);  // sets this thread's tmfwm_last_error(); returns code
+void clear_error();
+int check_frames(int64_t n, int32_t H, int32_t W, int64_t stride, int32_t block);
+
 hipError_t launch_embed(const EmbedArgs &a, hipStream_t st);
 hipError_t launch_edges(const uint8_t *src, uint8_t *dst, int64_t nframes, int H, int W, int64_t frame_stride, int block, hipStream_t st);
 hipError_t launch_extract(const ExtractArgs &a, hipStream_t st);
