@@ -316,21 +316,31 @@ def run(args, kernels=None, device=None):
     copy_gbs = measured_copy_peak(torch, dev) if rank == 0 and on_gpu else None
     build = lib_build_id() if on_gpu else None
 
+    # HBM bytes of the embed launch: counted FETCH / WRITE bytes per frame of this build and
+    # shape (profiles/valu.json, tools/pmc_embed.sh) x frames; else the older traffic.json
     traffic = None
-    tj = _profile_json("traffic.json")
-    if tj and (tj.get("build_id") in (None, build)):
-        traffic = tj.get("embed_kernel_hbm_bytes_per_launch", {}).get(f"{F}x{H}x{W}_b{b}")
-
-    valu = {}
     vj = _profile_json("valu.json")
-    if vj and H == 2160 and W == 3840 and vj.get("build_id") == build:
+    ek = (vj or {}).get("kernels", {}).get(f"embed_kernel<{b}>", {})
+    if vj and vj.get("build_id") == build and (ek.get("height"), ek.get("width")) == (H, W) and ek.get("hbm_bytes_per_frame"):
+        traffic = int(ek["hbm_bytes_per_frame"] * F)
+    else:
+        tj = _profile_json("traffic.json")
+        if tj and (tj.get("build_id") in (None, build)):
+            traffic = tj.get("embed_kernel_hbm_bytes_per_launch", {}).get(f"{F}x{H}x{W}_b{b}")
+
+    # VALU-issue roofline (tools/valu.py -> profiles/valu.json, counters of THIS build): the
+    # spec-rate issue cycles per frame over this run's cycles per frame at the clock the
+    # counter pass measured (GRBM_GUI_ACTIVE), i.e. the fraction of peak VALU issue
+    valu = {}
+    if vj and vj.get("build_id") == build:
         for name, ms in ((f"embed_kernel<{b}>", embed_ms), (f"extract_kernel<{b}>", extract_ms)):
             k = vj.get("kernels", {}).get(name)
-            if k:
-                bound = k["valu_issue_bound_us_per_frame"]
+            if k and (k.get("height"), k.get("width")) == (H, W) and k.get("clock_MHz"):
                 got = ms * 1e3 / F
-                valu[name] = {"bound_us_per_frame": bound, "us_per_frame": round(got, 2),
-                              "issue_fraction": round(bound / got, 3), "clock_MHz": k.get("clock_MHz")}
+                frac = k["issue_bound_cycles_per_frame"] / (got * k["clock_MHz"])
+                valu[name] = {"valu_instr_per_wave": k["valu_instr_per_wave"], "f64_per_wave": k["f64_arith_per_wave"],
+                              "bound_us_per_frame_at_clock": k["valu_issue_bound_us_per_frame"],
+                              "clock_MHz": k["clock_MHz"], "us_per_frame": round(got, 2), "issue_fraction": round(frac, 3)}
 
     if rank == 0:
         is4k = (H, W) == (2160, 3840)

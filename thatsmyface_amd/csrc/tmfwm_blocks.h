@@ -183,8 +183,11 @@ TMF_DEVI void luma_rows(const uint32_t (&words)[Geo<B>::R][Geo<B>::NW], float (&
 // then fits b <= 10 and 14 into 2-3 waves, but b = 12 and 16 overflow into AGPRs and run
 // one wave per SIMD).  Forcing 2 for b = 12 / 16 costs 156 / 256 B of scratch per lane
 // and is faster: embed<12> 283 -> 201 us, embed<16> 531 -> 345 us per 4K frame.
+#ifndef TMF_EMBED8_WAVES
+#define TMF_EMBED8_WAVES 1
+#endif
 template <int B>
-constexpr int kEmbedWaves = (B == 12 || B == 16) ? TMF_EMBED_WAVES_BIG : 1;
+constexpr int kEmbedWaves = (B == 12 || B == 16) ? TMF_EMBED_WAVES_BIG : B == 8 ? TMF_EMBED8_WAVES : 1;
 
 template <int B>
 __global__ __launch_bounds__(64, kEmbedWaves<B>) void embed_kernel(EmbedArgs a)

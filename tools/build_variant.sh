@@ -1,18 +1,20 @@
 #!/bin/bash
 # Build an experimental library variant: tools/build_variant.sh <name> [extra hipcc flags...]
 # -> variants/libtmfwm_<name>.so (git-ignored; travels to the GPU box; load it with TMFWM_LIB).
+# Only the kernel TUs take the extra flags; the ABI / tile / dgesdd-route objects are the
+# main build's (make -C thatsmyface_amd/csrc first).
 set -euo pipefail
 NAME=$1; shift
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 C=$ROOT/thatsmyface_amd/csrc
+make -s -C "$C" >/dev/null
 T=$(mktemp -d)
 F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -fno-slp-vectorize -Wall $*"
 /opt/rocm/bin/hipcc $F -c "$C/tmfwm_kernels.hip" -o "$T/k.o" &
 /opt/rocm/bin/hipcc $F -mllvm -amdgpu-sched-strategy=max-ilp -c "$C/tmfwm_embed8.hip" -o "$T/e8.o" &
-/opt/rocm/bin/hipcc $F -x hip -c "$C/tmfwm_capi.cpp" -o "$T/c.o" &
-/opt/rocm/bin/hipcc $F -c "$C/tmfwm_tile.hip" -o "$T/t.o" &
 wait
 mkdir -p "$ROOT/variants"
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$ROOT/variants/libtmfwm_$NAME.so" "$T/k.o" "$T/e8.o" "$T/c.o" "$T/t.o"
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$ROOT/variants/libtmfwm_$NAME.so" "$T/k.o" "$T/e8.o" \
+    "$C/tmfwm_capi.o" "$C/tmfwm_multi.o" "$C/tmfwm_tile.o" "$C/tmfwm_fallback.o" -ldl -lpthread
 rm -rf "$T"
 echo "variants/libtmfwm_$NAME.so"

@@ -1,16 +1,24 @@
 #!/usr/bin/env python3
-"""VALU-issue roofline of the embed / extract kernels from SQ instruction counters.
+"""VALU-issue roofline of the embed / extract kernels from rocprofv3 counters.
 
-Inputs: tools/pmc_embed.sh output directories (three rocprofv3 --pmc passes over
-tools/time_embed.py) and the issue costs measured by tools/micro/chain_rate.hip on
-MI355X (profiles/r01e_valu_chain_rate.log): with enough independent work per SIMD an
-f64 FMA issues every ~5.0 cycles and an f32 FMA every ~2.8 cycles (2.4 GHz clock).
-Every f64 arithmetic instruction (SQ_INSTS_VALU_{FMA,MUL,ADD,TRANS}_F64) is priced at
-the f64 cost, every other VALU instruction at the f32 cost.  The estimate is the time
-one SIMD needs to ISSUE its share of the frame's waves; bench.py divides it by the
-measured launch time (fraction of the VALU-issue bound).
+Input: one tools/pmc_embed.sh output directory (passes p1-p6 over tools/time_embed.py at
+one block size, recorded in <dir>/block).  For the timed (last) dispatch of each kernel:
 
-Usage: python tools/valu.py <pmc_dir> --frames 16 --height 2160 --width 3840 --block 8 --out profiles/valu.json
+* instruction mix per wave (SQ_INSTS_VALU and its f64 / transcendental classes);
+* issue cycles per wave at the SPEC rates of a gfx950 SIMD-32 (MI355X_MICROARCH.md: a
+  wave64 VALU instruction issues over 2 cycles; FP64 vector is half rate, 78.6 vs 157.3
+  TFLOP/s, so 4 cycles for f64 FMA / MUL / ADD; a transcendental costs twice a plain op
+  in the guide's issue-cost row, 4 cycles f32; f64 transcendentals priced at 8 -- that
+  class is not in the guide, so the bound is approximate there, ~1 % of embed's mix);
+* the effective clock of that dispatch, GRBM_GUI_ACTIVE / 8 XCDs / its duration (guide,
+  'DVFS give-back'), and the bound in microseconds per frame at that clock;
+* HBM bytes per frame from FETCH_SIZE (x2, gfx950) and WRITE_SIZE (KB).
+
+The bound is a floor: a kernel that issued VALU work back to back on every SIMD at the
+spec rate would take that long.  bench.py reports bound / measured (issue fraction).
+
+Usage: python tools/valu.py <pmc_dir> [--height 2160 --width 3840] --build <lib hash> --out profiles/valu.json
+Entries for other block sizes already in --out (same build) are kept.
 """
 import argparse
 import csv
@@ -18,52 +26,86 @@ import glob
 import json
 import os
 
-F64_CYC, OTHER_CYC, CLOCK_HZ, SIMDS = 5.0, 2.8, 2.4e9, 1024
-F64 = ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_TRANS_F64")
+SIMDS, XCDS = 1024, 8
+CYC = {"plain": 2.0, "f64": 4.0, "trans_f32": 4.0, "trans_f64": 8.0}
+F64 = ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64")
 
 
-def per_wave(d, kernel):
-    agg = {}
-    for f in glob.glob(os.path.join(d, "p*", "p_counter_collection.csv")):
+def last_dispatch(d, kernel):
+    """counter -> value and (start, end) ns of the last dispatch of `kernel`, over all passes."""
+    agg, span = {}, {}
+    for f in sorted(glob.glob(os.path.join(d, "p*", "**", "*counter_collection.csv"), recursive=True)):
         disp = {}
         for r in csv.DictReader(open(f)):
             if kernel in r["Kernel_Name"]:
-                disp.setdefault(int(r["Dispatch_Id"]), {})
-                c = disp[int(r["Dispatch_Id"])]
+                k = int(r["Dispatch_Id"])
+                c = disp.setdefault(k, {})
                 c[r["Counter_Name"]] = c.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+                span[(f, k)] = (int(r["Start_Timestamp"]), int(r["End_Timestamp"]))
         if disp:
-            agg.update(disp[max(disp)])  # the timed (last) dispatch
-    waves = agg["SQ_WAVES"]
-    return {k: v / waves for k, v in agg.items() if k != "SQ_WAVES"}, waves
+            k = max(disp)
+            agg.update(disp[k])
+            if "GRBM_GUI_ACTIVE" in disp[k]:
+                agg["_ns"] = span[(f, k)][1] - span[(f, k)][0]
+    return agg
 
 
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("pmc_dir")
-    p.add_argument("--frames", type=int, default=16)
     p.add_argument("--height", type=int, default=2160)
     p.add_argument("--width", type=int, default=3840)
-    p.add_argument("--block", type=int, default=8)
+    p.add_argument("--build", default=None, help="sha256 prefix of the measured libtmfwm.so (bench.py lib_build)")
     p.add_argument("--out", default="profiles/valu.json")
     a = p.parse_args()
-    out = {"source": f"{a.pmc_dir} (tools/pmc_embed.sh, {a.frames} frames {a.width}x{a.height}, b={a.block})",
-           "issue_cost_cycles": {"f64_arith": F64_CYC, "other_valu": OTHER_CYC,
-                                 "from": "tools/micro/chain_rate.hip, profiles/r01e_valu_chain_rate.log"},
-           "clock_hz": CLOCK_HZ, "simds": SIMDS, "kernels": {}}
+    block, frames = (int(v) for v in open(os.path.join(a.pmc_dir, "block")).read().split())
+    out = {}
+    if os.path.exists(a.out):
+        old = json.load(open(a.out))
+        if old.get("build_id") == a.build and "spec_issue_cycles" in old:
+            out = old
+    out.update({
+        "build_id": a.build,
+        "spec_issue_cycles": CYC,
+        "model": "issue cycles per wave at the gfx950 spec rates (tools/valu.py docstring); effective clock from "
+                 "GRBM_GUI_ACTIVE / 8 / dispatch time; HBM bytes = 2 x FETCH_SIZE + WRITE_SIZE",
+    })
+    out.setdefault("kernels", {})
+    H, W = a.height, a.width
     for k in ("embed_kernel", "extract_kernel"):
-        pw, waves = per_wave(a.pmc_dir, k)
-        f64 = sum(pw.get(c, 0.0) for c in F64)
+        c = last_dispatch(a.pmc_dir, f"{k}<{block}>")
+        waves = c["SQ_WAVES"]
+        pw = {n: v / waves for n, v in c.items() if n.startswith("SQ_") and n != "SQ_WAVES"}
         valu = pw["SQ_INSTS_VALU"]
-        cyc = f64 * F64_CYC + (valu - f64) * OTHER_CYC
-        wpf = waves / a.frames
-        us = cyc * wpf / SIMDS / CLOCK_HZ * 1e6
-        out["kernels"][f"{k}<{a.block}>"] = {
-            "valu_instr_per_wave": round(valu, 1), "f64_instr_per_wave": round(f64, 1),
-            "waves_per_frame": wpf, "issue_cycles_per_wave": round(cyc, 1),
-            "valu_issue_bound_us_per_frame": round(us, 2)}
+        f64 = sum(pw.get(n, 0.0) for n in F64)
+        t32, t64 = pw.get("SQ_INSTS_VALU_TRANS_F32", 0.0), pw.get("SQ_INSTS_VALU_TRANS_F64", 0.0)
+        plain = valu - f64 - t32 - t64
+        cyc = plain * CYC["plain"] + f64 * CYC["f64"] + t32 * CYC["trans_f32"] + t64 * CYC["trans_f64"]
+        wpf = waves / frames
+        ns = c.get("_ns")
+        clock = c["GRBM_GUI_ACTIVE"] / XCDS / (ns * 1e-9) if ns else None
+        bound_cyc_frame = cyc * wpf / SIMDS
+        ent = {
+            "frames": frames, "height": H, "width": W,
+            "valu_instr_per_wave": round(valu, 1), "f64_arith_per_wave": round(f64, 1),
+            "trans_f32_per_wave": round(t32, 1), "trans_f64_per_wave": round(t64, 1),
+            "salu_per_wave": round(pw.get("SQ_INSTS_SALU", 0.0), 1), "lds_per_wave": round(pw.get("SQ_INSTS_LDS", 0.0), 1),
+            "waves_per_frame": wpf,
+            "issue_cycles_per_wave": round(cyc, 1),
+            "issue_bound_cycles_per_frame": round(bound_cyc_frame),
+            "profiled_us_per_frame": round(ns * 1e-3 / frames, 2) if ns else None,
+            "clock_MHz": round(clock / 1e6) if clock else None,
+            "valu_issue_bound_us_per_frame": round(bound_cyc_frame / clock * 1e6, 2) if clock else None,
+            "wait_inst_any_frac": round(pw["SQ_WAIT_INST_ANY"] / pw["SQ_WAVE_CYCLES"], 3) if "SQ_WAVE_CYCLES" in pw else None,
+        }
+        if ns and clock:
+            ent["issue_fraction_profiled"] = round(ent["valu_issue_bound_us_per_frame"] / ent["profiled_us_per_frame"], 3)
+        if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+            ent["hbm_bytes_per_frame"] = round((2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024 / frames)
+        out["kernels"][f"{k}<{block}>"] = ent
     with open(a.out, "w") as f:
         json.dump(out, f, indent=1)
-    print(json.dumps(out["kernels"], indent=1))
+    print(json.dumps({n: v for n, v in out["kernels"].items() if n.endswith(f"<{block}>")}, indent=1))
 
 
 if __name__ == "__main__":
