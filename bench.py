@@ -56,6 +56,9 @@ def parse(argv=None):
     p.add_argument("--cpu-frames", type=int, default=48,
                    help="frames in the CPU-baseline / parity sample, ~10-20 s of oracle work on 16 cores (0 = skip)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--structured-crops", type=int, default=16,
+                   help="block-aligned 960x544 crops timed with the reference's cost model (oracle/structured.py), "
+                        "one per host core; 0 = skip")
     p.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                    help="process-group backend for N > 1 (nccl = RCCL over xGMI; gloo only to rehearse "
                         "several ranks on one GPU)")
@@ -191,6 +194,7 @@ def lib_build_id():
 def run(args, kernels=None, device=None):
     """One rank of the benchmark.  `kernels` / `device` default to the HIP path on this
     rank's GPU; the CPU test of the multi-rank code substitutes its own (tests/)."""
+    import numpy as np
     import torch
     import torch.distributed as dist
 
@@ -313,6 +317,34 @@ def run(args, kernels=None, device=None):
         parity = {"frames": checked, "embed_mismatch": bad_e, "extract_mismatch": bad_x,
                   "summary": f"{checked - max(bad_e, bad_x)}/{checked} frames bit-exact vs oracle"}
 
+    # the reference's own cost model: per-pixel np.dot colour loops and
+    # per-block scipy / LAPACK calls (oracle/structured.py) on block-aligned crops of the
+    # batch's first frames, one single-threaded process per host core; each crop's bytes are
+    # compared with the same region of the GPU's output (equal where this host's OpenBLAS
+    # core is the reference's SkylakeX)
+    structured = None
+    if want_cpu and args.structured_crops > 0:
+        from oracle import structured as ST
+
+        ch, cw = min(H, 68 * b), min(W, 120 * b)
+        k = min(args.structured_crops, n_local)
+        idx = list(range(k))
+        covers = list(frames[idx, :ch, :cw].cpu().numpy())
+        tiles = [wm[: ch // b, : cw // b].cpu().numpy()] * k
+        res, wall = ST.run_pool(covers, tiles, b, alpha, oracle_threads(1))
+        gout = rt.out[idx, :ch, :cw].cpu().numpy()
+        gext = rt.tiles[idx, : ch // b, : cw // b].cpu().numpy()
+        same = sum(int(np.array_equal(r[1], gout[i]) and np.array_equal(r[2], gext[i])) for i, r in enumerate(res))
+        structured = {
+            "value": round(k * ch * cw / wall / 1e6, 4),
+            "unit": "Mpixels/s",
+            "cores": oracle_threads(1),
+            "kind": "reference cost model (oracle/structured.py: the reference's per-pixel np.dot and per-block "
+                    "scipy.fftpack / np.linalg.svd loops, one single-threaded process per core)",
+            "sample": f"{k} crops of {cw}x{ch} from the batch's first {k} frames, embed+extract, {wall:.2f} s wall",
+            "per_crop_s": round(sum(r[0] for r in res) / k, 2),
+            "crops_bit_exact_vs_gpu": f"{same}/{k}",
+        }
     copy_gbs = measured_copy_peak(torch, dev) if rank == 0 and on_gpu else None
     build = lib_build_id() if on_gpu else None
 
@@ -390,6 +422,7 @@ def run(args, kernels=None, device=None):
                            "extract_valu_issue": valu.get(f"extract_kernel<{b}>")},
             "parity_sample": parity,
             "cpu_baseline": cpu,
+            "cpu_baseline_reference_model": structured,
             "lib_build": build,
         }
         if world > 1 and args.backend == "gloo":

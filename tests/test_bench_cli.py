@@ -66,3 +66,28 @@ def test_bench_two_ranks_gloo(tmp_path, capfd):
         gotx[s:s + len(z["tiles"])] = z["tiles"]
     assert np.array_equal(got, ref)
     assert np.array_equal(gotx, refx)
+
+
+def test_bench_one_rank_cpu_baselines(tmp_path, capfd):
+    """N = 1: the oracle CPU baseline + parity sample and the reference-cost-model baseline
+    (oracle/structured.py on block-aligned crops) both run and report; with oracle kernels
+    standing in for the GPU the crops must be bit-exact on this host's OpenBLAS core."""
+    import subprocess
+    import sys
+
+    F, H, W, B = 2, 48, 80, 8
+    env = dict(os.environ, TMF_BENCH_DUMP=str(tmp_path))
+    env.pop("WORLD_SIZE", None)
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "bench_rank_cpu.py"), "--frames", str(F), "--height",
+                          str(H), "--width", str(W), "--steps", "1", "--warmup", "0", "--cpu-frames", "2",
+                          "--structured-crops", "2"], env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    line = json.loads([x for x in out.stdout.splitlines() if x.startswith("{")][-1])
+    assert line["parity_sample"]["frames"] == 2 and line["parity_sample"]["embed_mismatch"] == 0
+    assert line["cpu_baseline"]["kind"] == "port" and line["cpu_baseline"]["value"] > 0
+    rm = line["cpu_baseline_reference_model"]
+    assert rm["value"] > 0 and rm["crops_bit_exact_vs_gpu"].endswith("/2")
+    from test_oracle_lapack import _CORE
+
+    if _CORE == "SkylakeX":
+        assert rm["crops_bit_exact_vs_gpu"] == "2/2"

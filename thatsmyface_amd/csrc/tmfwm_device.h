@@ -701,34 +701,6 @@ TMF_DEVI T group_sum(T v)
     return v;
 }
 
-// 8-lane broadcast of lane K by two DPP moves (no LDS pipe): quad_perm [k,k,k,k] (k = K & 3)
-// gives every quad its own lane k; then the other half of each 8-lane group copies the
-// half that holds lane K -- row_shr:4 into banks 1 and 3 (K < 4) or row_shl:4 into banks
-// 0 and 2 (K >= 4); lanes of the other banks keep their value (update_dpp's `old`).
-#ifndef TMF_BCAST8_DPP
-#define TMF_BCAST8_DPP 0
-#endif
-#ifndef TMF_BCAST_BATCH
-#define TMF_BCAST_BATCH 0
-#endif
-template <int K>
-TMF_DEVI int bcast8_i(int v)
-{
-    constexpr int k = K & 3;
-    const int x = __builtin_amdgcn_mov_dpp(v, k | (k << 2) | (k << 4) | (k << 6), 0xF, 0xF, false);
-    if constexpr (K < 4) return __builtin_amdgcn_update_dpp(x, x, 0x114, 0xF, 0xA, false);
-    else return __builtin_amdgcn_update_dpp(x, x, 0x104, 0xF, 0x5, false);
-}
-template <int K>
-TMF_DEVI double bcast8(double v)
-{
-    const long long b = __builtin_bit_cast(long long, v);
-    const int lo = bcast8_i<K>((int)b), hi = bcast8_i<K>((int)(b >> 32));
-    return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
-}
-template <int K>
-TMF_DEVI float bcast8(float v) { return __builtin_bit_cast(float, bcast8_i<K>(__builtin_bit_cast(int, v))); }
-
 // value of lane (group base + K) for every lane of the group
 template <int L, int K, typename T>
 TMF_DEVI T group_bcast(T v)
@@ -736,7 +708,6 @@ TMF_DEVI T group_bcast(T v)
     if constexpr (L == 1) return v;
     else if constexpr (L == 2) return dpp<K == 0 ? 0xA0 : 0xF5>(v);                    // quad_perm [K,K,K+2,K+2]
     else if constexpr (L == 4) return dpp<K | (K << 2) | (K << 4) | (K << 6)>(v);      // quad_perm [K,K,K,K]
-    else if constexpr (TMF_BCAST8_DPP) return bcast8<K>(v);
     else return swz<(K << 5) | 0x18>(v);                                                // bitmask: (lane & 0x18) | K
 }
 
@@ -955,21 +926,11 @@ TMF_DEVI int jacobi(T (&A)[(B + L - 1) / L][B], T (&V)[(B + L - 1) / L][B], int 
                     mine[U].tg = o ? r.tg : T(0);
                 }
             });
-            // TMF_BCAST_BATCH: all of the round's broadcasts first, then the updates (more
-            // registers, but no update waits on the broadcast just before it)
-            T bc[TMF_BCAST_BATCH ? NP : 1], bs[TMF_BCAST_BATCH ? NP : 1], bt[TMF_BCAST_BATCH ? NP : 1];
-            if constexpr (TMF_BCAST_BATCH)
-                static_for<NP>([&](auto Pi) {
-                    constexpr int p = Pi, u = p % PP, src = p / PP;
-                    bc[p] = group_bcast<L, src>(mine[u].c);
-                    bs[p] = group_bcast<L, src>(mine[u].s);
-                    bt[p] = group_bcast<L, src>(mine[u].tg);
-                });
             static_for<NP>([&](auto Pi) {
                 constexpr int p = Pi, i = Sched<B>::lo(s, p), j = Sched<B>::hi(s, p), u = p % PP, src = p / PP;
-                const T c = TMF_BCAST_BATCH ? bc[TMF_BCAST_BATCH ? p : 0] : group_bcast<L, src>(mine[u].c);
-                const T sn = TMF_BCAST_BATCH ? bs[TMF_BCAST_BATCH ? p : 0] : group_bcast<L, src>(mine[u].s);
-                const T tg = TMF_BCAST_BATCH ? bt[TMF_BCAST_BATCH ? p : 0] : group_bcast<L, src>(mine[u].tg);
+                const T c = group_bcast<L, src>(mine[u].c);
+                const T sn = group_bcast<L, src>(mine[u].s);
+                const T tg = group_bcast<L, src>(mine[u].tg);
                 // Wave-uniform branch (taken iff the owner lane of this pair rotates it in
                 // some block of the wave); lanes whose block skips this pair apply the identity
                 // (c, s, t*gamma) = (1, 0, 0): fma(-0, y, 1*x) == x bitwise for every value
