@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define TMFWM_ABI_VERSION 3
+#define TMFWM_ABI_VERSION 4
 
 #define TMFWM_MEM_HOST 0
 #define TMFWM_MEM_DEVICE 1
@@ -51,6 +51,7 @@ extern "C" {
 #define TMFWM_ERR_HIP (-5)          /* HIP runtime / launch error (EIO) */
 #define TMFWM_ERR_UNSUPPORTED (-95) /* block size not an even 4..16 (EOPNOTSUPP) */
 #define TMFWM_ERR_NODEVICE (-19)    /* no usable gfx950 device (ENODEV) */
+#define TMFWM_ERR_NODATA (-61)      /* no decodable QR code in the image (ENODATA) */
 
 /* ABI version (TMFWM_ABI_VERSION) compiled into the library. */
 int tmfwm_abi_version(void);
@@ -169,6 +170,43 @@ int tmfwm_synth_frames(uint64_t seed, int64_t frame0, int64_t n_frames, int64_t 
  */
 int tmfwm_prepare_tile(const uint8_t *wm, int32_t wm_height, int32_t wm_width, int32_t tile_height, int32_t tile_width,
                        int32_t preserve_ratio, uint8_t *tile, int32_t mem_kind, void *hip_stream);
+
+/*
+ * The watermark's payload, host-side C++ (no GPU, no torch): the QR codec
+ * and AES-CBC the app wraps around embed / extract.  The reference builds the watermark with
+ * modules/encryption.py:8-40 (encrypt_watermark: random 16-byte IV + AES-CBC of the
+ * PKCS#7-padded text) and modules/qrcode_generator.py:10-44 (text_to_qrcode: base64 text,
+ * python-qrcode ERROR_CORRECT_H, version >= 1 fitted, box 10, border 4, 300 x 300), and reads
+ * it back with qrcode_to_text (:47-76, pyzbar) and decrypt_watermark (encryption.py:43-68,
+ * pycryptodome) at internal_pages/extract_watermark_page.py:356-364.
+ *
+ * tmfwm_qr_encode: data -> size x size modules (1 = dark, row-major) of the smallest version
+ * >= min_version (1..10) that fits at ec_level (0 L, 1 M, 2 Q, 3 H), segmented and masked as
+ * python-qrcode does (mask = -1: lowest penalty; 0..7 forces one).  *size_out = 17 + 4 v
+ * (also on a too-small buffer, TMFWM_ERR_INVALID).  Data beyond version 10: TMFWM_ERR_UNSUPPORTED.
+ */
+int tmfwm_qr_encode(const uint8_t *data, int32_t len, int32_t ec_level, int32_t min_version, int32_t mask, uint8_t *modules,
+                    int32_t capacity, int32_t *size_out);
+
+/* tmfwm_qr_decode: an upright QR symbol (versions 1..10) in an 8-bit grey image (dark =
+ * low), e.g. an extracted watermark tile, -> its payload bytes (numeric, alphanumeric and
+ * byte segments, Reed-Solomon corrected).  TMFWM_ERR_NODATA when no symbol decodes;
+ * *len_out = payload length (also when capacity is too small: TMFWM_ERR_INVALID). */
+int tmfwm_qr_decode(const uint8_t *gray, int32_t height, int32_t width, int64_t row_stride, uint8_t *out, int32_t capacity,
+                    int32_t *len_out);
+
+/* tmfwm_qr_decode over n_tiles back-to-back height x width tiles (tmfwm_extract's output
+ * layout), on host threads: payload of tile i at out + i*capacity, lens[i] = its length or
+ * -1 when the tile holds no decodable symbol (or it exceeds capacity). */
+int tmfwm_qr_decode_batch(const uint8_t *tiles, int64_t n_tiles, int32_t height, int32_t width, uint8_t *out, int32_t capacity,
+                          int32_t *lens);
+
+/* AES-CBC (FIPS-197, SP 800-38A) with a 16 / 24 / 32-byte key and a 16-byte IV over len bytes
+ * (a multiple of 16; padding is the caller's: PKCS#7 in the app).  out may equal in. */
+int tmfwm_aes_cbc_encrypt(const uint8_t *key, int32_t key_len, const uint8_t *iv, const uint8_t *in, int64_t len,
+                          uint8_t *out);
+int tmfwm_aes_cbc_decrypt(const uint8_t *key, int32_t key_len, const uint8_t *iv, const uint8_t *in, int64_t len,
+                          uint8_t *out);
 
 #ifdef __cplusplus
 }

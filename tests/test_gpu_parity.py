@@ -593,3 +593,39 @@ def test_multi_entry_points_logical_shards(dev, monkeypatch):
             assert np.array_equal(out[f], ref), (shards, f)
             assert np.array_equal(ext[f], O.extract_frame(ref, host[f], b, 0.1)), (shards, f)
     assert torch.cuda.current_device() == 0
+
+
+def test_payload_round_trip_dropin_gpu(dev):
+    """The app's full loop on the GPU path (embed_watermark_page.py:480-531 ->
+    extract_watermark_page.py:293-364): encrypt -> text_to_qrcode -> PNG bytes ->
+    embed_watermark(preserve_ratio=True) | extract_watermark -> qrcode_to_text ->
+    decrypt_watermark; and a batch of extracted tiles decoded on host threads."""
+    import io
+
+    from lapack_path import photo_cover
+
+    from thatsmyface_amd import batch
+    from thatsmyface_amd import encryption as E
+    from thatsmyface_amd import qrcode_generator as Q
+    from thatsmyface_amd import watermarking as W
+
+    key = bytes(range(7, 39))
+    enc = E.encrypt_watermark("ThatsMyFace on MI355X", key)
+    buf = io.BytesIO()
+    Q.text_to_qrcode(enc).save(buf, format="PNG")
+    cov = Image.fromarray(photo_cover(1080, 1920, 4))
+    for b in (8, 16):
+        st = {"block_size": b, "alpha": 0.1}
+        emb = W.embed_watermark(cov, buf.getvalue(), True, st)
+        ext = W.extract_watermark(emb, cov, st)
+        got = Q.qrcode_to_text(ext)
+        assert got == enc, b
+        assert E.decrypt_watermark(got, key) == "ThatsMyFace on MI355X".encode()
+    # batch: 4 frames, one tile, extracted on the GPU, decoded on the host
+    frames = torch.from_numpy(np.stack([photo_cover(1080, 1920, s) for s in range(4)])).to(dev)
+    wm = np.asarray(Image.open(io.BytesIO(buf.getvalue())).convert("L"))
+    tile = batch.prepare_tile(torch.from_numpy(wm).to(dev), 1080 // 8, 1920 // 8, True)
+    tiles = batch.extract_batch(batch.embed_batch(frames, tile, 8, 0.1), frames, 8, 0.1)
+    import base64
+
+    assert Q.decode_tiles(tiles.cpu().numpy()) == [base64.b64encode(enc)] * 4

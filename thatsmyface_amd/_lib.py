@@ -14,7 +14,7 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # TMFWM_LIB selects an alternative build (e.g. the phase-profile libtmfwm_stamps.so)
 LIB_PATH = os.environ.get("TMFWM_LIB") or os.path.join(_HERE, "libtmfwm.so")
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 MEM_HOST = 0
 MEM_DEVICE = 1
@@ -24,6 +24,7 @@ ERR_NOMEM = -12
 ERR_HIP = -5
 ERR_UNSUPPORTED = -95
 ERR_NODEVICE = -19
+ERR_NODATA = -61
 
 _u8p = ctypes.c_void_p
 _I64 = ctypes.c_int64
@@ -50,6 +51,11 @@ SIGNATURES = {
     "tmfwm_lapack_nrm2": (ctypes.c_int, [_VP, _I64, _I32, _I32, _VP, _I32, _VP]),
     "tmfwm_synth_frames": (ctypes.c_int, [ctypes.c_uint64, _I64, _I64, _I64, _VP, _VP]),
     "tmfwm_prepare_tile": (ctypes.c_int, [_VP, _I32, _I32, _I32, _I32, _I32, _VP, _I32, _VP]),
+    "tmfwm_qr_encode": (ctypes.c_int, [_VP, _I32, _I32, _I32, _I32, _VP, _I32, _VP]),
+    "tmfwm_qr_decode": (ctypes.c_int, [_VP, _I32, _I32, _I64, _VP, _I32, _VP]),
+    "tmfwm_qr_decode_batch": (ctypes.c_int, [_VP, _I64, _I32, _I32, _VP, _I32, _VP]),
+    "tmfwm_aes_cbc_encrypt": (ctypes.c_int, [_VP, _I32, _VP, _VP, _I64, _VP]),
+    "tmfwm_aes_cbc_decrypt": (ctypes.c_int, [_VP, _I32, _VP, _VP, _I64, _VP]),
 }
 
 _lock = threading.Lock()
