@@ -613,8 +613,8 @@ def test_payload_round_trip_dropin_gpu(dev):
     enc = E.encrypt_watermark("ThatsMyFace on MI355X", key)
     buf = io.BytesIO()
     Q.text_to_qrcode(enc).save(buf, format="PNG")
-    cov = Image.fromarray(photo_cover(1080, 1920, 4))
-    for b in (8, 16):
+    for b, (h, w) in ((8, (1080, 1920)), (16, (2160, 3840))):  # >= 2 tile pixels per QR module
+        cov = Image.fromarray(photo_cover(h, w, 4))
         st = {"block_size": b, "alpha": 0.1}
         emb = W.embed_watermark(cov, buf.getvalue(), True, st)
         ext = W.extract_watermark(emb, cov, st)
@@ -623,7 +623,7 @@ def test_payload_round_trip_dropin_gpu(dev):
         assert E.decrypt_watermark(got, key) == "ThatsMyFace on MI355X".encode()
     # batch: 4 frames, one tile, extracted on the GPU, decoded on the host
     frames = torch.from_numpy(np.stack([photo_cover(1080, 1920, s) for s in range(4)])).to(dev)
-    wm = np.asarray(Image.open(io.BytesIO(buf.getvalue())).convert("L"))
+    wm = np.array(Image.open(io.BytesIO(buf.getvalue())).convert("L"))
     tile = batch.prepare_tile(torch.from_numpy(wm).to(dev), 1080 // 8, 1920 // 8, True)
     tiles = batch.extract_batch(batch.embed_batch(frames, tile, 8, 0.1), frames, 8, 0.1)
     import base64

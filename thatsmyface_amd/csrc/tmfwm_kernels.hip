@@ -24,7 +24,10 @@ extern template __global__ void embed_kernel<8>(EmbedArgs);  // tmfwm_embed8.hip
 #ifndef TMF_POWER_ITERS
 #define TMF_POWER_ITERS 6
 #endif
-constexpr int kPowerIters = TMF_POWER_ITERS;  // f32 power iterations before certification
+constexpr int kPowerIters = TMF_POWER_ITERS;
+#ifndef TMF_EXTRACT8_WAVES
+#define TMF_EXTRACT8_WAVES 3
+#endif  // f32 power iterations before certification
 
 template <int B>
 TMF_DEVI bool sigma1_of(const uint32_t (&words)[Geo<B>::R][Geo<B>::NW], int q, float *tile, float &s1)
@@ -37,7 +40,7 @@ TMF_DEVI bool sigma1_of(const uint32_t (&words)[Geo<B>::R][Geo<B>::NW], int q, f
 }
 
 template <int B>
-__global__ __launch_bounds__(64, (B > 8 ? 2 : 3)) void extract_kernel(ExtractArgs a)  // waves per SIMD
+__global__ __launch_bounds__(64, (B > 8 ? 2 : TMF_EXTRACT8_WAVES)) void extract_kernel(ExtractArgs a)  // waves per SIMD
 {
     constexpr int L = Geo<B>::L, BPW = Geo<B>::BPW, LD = B + 1;
     __shared__ float lds[BPW * B * LD];

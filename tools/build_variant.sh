@@ -15,6 +15,6 @@ F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -
 wait
 mkdir -p "$ROOT/variants"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$ROOT/variants/libtmfwm_$NAME.so" "$T/k.o" "$T/e8.o" \
-    "$C/tmfwm_capi.o" "$C/tmfwm_multi.o" "$C/tmfwm_tile.o" "$C/tmfwm_fallback.o" -ldl -lpthread
+    "$C/tmfwm_capi.o" "$C/tmfwm_multi.o" "$C/tmfwm_qr.o" "$C/tmfwm_tile.o" "$C/tmfwm_fallback.o" -fopenmp -ldl -lpthread
 rm -rf "$T"
 echo "variants/libtmfwm_$NAME.so"
