@@ -729,82 +729,6 @@ static void rotationf(float alpha, float beta, float gamma, float *c, float *s, 
     *tg = (((g * g) * r) * (q * q)) * sg;
 }
 
-/* Small-angle rotations.  Once the f32 phase has preconditioned the
- * block, almost every pair has |g| tiny against |d| (rho = g/|d| ~ 1e-7 .. 1e-14 in the
- * f64 phase), and t = tan(theta) = sgn(d) g / (|d| + sqrt(d^2 + g^2)) has the series
- * sgn(d) (rho/2) (1 - rho^2/4 + rho^4/8 - ...).  For |g| <= 2^-13 |d| the first two terms
- * are exact to 2^-55 relative; c = fma(-t/2, t, 1) is 1/sqrt(1 + t^2) to 3t^4/8 <= 2^-57,
- * so c^2 + s^2 = 1 to rounding with s = c t; t*gamma updates the norms as before.  1/|d|
- * comes from an integer seed (0x7fde623822fc16e6 - bits, relative error <= 5.1 %) and
- * three Newton steps e = fma(-x, y, 1), y = fma(y, e, y) (error 4.2e-11: t only steers
- * the convergence, the rotation is orthogonal whatever its angle).  17 f64 operations
- * against ~42 for rotation().  f32 twin: |g| <= 2^-6 |d|, seed 0x7ef311c7, two steps. */
-#define JAC_SMALL 0x1p-13
-#define JAC_DMIN 0x1p-1000
-#define JAC32_SMALL 0x1p-6f
-#define JAC32_DMIN 0x1p-100f
-
-static double rcp_n(double x) /* x > 0, normal */
-{
-    uint64_t i;
-    double y;
-    memcpy(&i, &x, 8);
-    i = 0x7fde623822fc16e6ull - i;
-    memcpy(&y, &i, 8);
-    for (int k = 0; k < 3; ++k) {
-        const double e = fma(-x, y, 1.0);
-        y = fma(y, e, y);
-    }
-    return y;
-}
-
-static float rcpf_n(float x)
-{
-    uint32_t i;
-    float y;
-    memcpy(&i, &x, 4);
-    i = 0x7ef311c7u - i;
-    memcpy(&y, &i, 4);
-    for (int k = 0; k < 2; ++k) {
-        const float e = fmaf(-x, y, 1.0f);
-        y = fmaf(y, e, y);
-    }
-    return y;
-}
-
-/* rotation() or its small-angle form, by the pair's own (d, g) */
-static void rotation_any(double alpha, double beta, double gamma, double *c, double *s, double *tg)
-{
-    const double d = beta - alpha, g = gamma + gamma, ad = fabs(d);
-    if (!(ad >= JAC_DMIN && fabs(g) <= JAC_SMALL * ad)) {
-        rotation(alpha, beta, gamma, c, s, tg);
-        return;
-    }
-    const double rho = g * rcp_n(ad);
-    const double h = fma(-0.25, rho * rho, 1.0);
-    const double t = (rho * h) * copysign(0.5, d);
-    const double cc = fma(-0.5 * t, t, 1.0);
-    *c = cc;
-    *s = cc * t;
-    *tg = t * gamma;
-}
-
-static void rotationf_any(float alpha, float beta, float gamma, float *c, float *s, float *tg)
-{
-    const float d = beta - alpha, g = gamma + gamma, ad = fabsf(d);
-    if (!(ad >= JAC32_DMIN && fabsf(g) <= JAC32_SMALL * ad)) {
-        rotationf(alpha, beta, gamma, c, s, tg);
-        return;
-    }
-    const float rho = g * rcpf_n(ad);
-    const float h = fmaf(-0.25f, rho * rho, 1.0f);
-    const float t = (rho * h) * copysignf(0.5f, d);
-    const float cc = fmaf(-0.5f * t, t, 1.0f);
-    *c = cc;
-    *s = cc * t;
-    *tg = t * gamma;
-}
-
 static float tree_sumf(float *v, int n)
 {
     while (n > 1) {
@@ -858,7 +782,7 @@ static int jacobi_f32(float *A, float *V, int b)
                 if (g2 <= c2a || g2 <= c2 * (alpha + beta) || g2 <= (JAC32_TOL2 * alpha) * beta) continue;
                 rotated = 1;
                 float c, sn, tg;
-                rotationf_any(alpha, beta, gamma, &c, &sn, &tg);
+                rotationf(alpha, beta, gamma, &c, &sn, &tg);
                 nrm[i] = alpha - tg;
                 nrm[j] = beta + tg;
                 for (int r = 0; r < b; ++r) {
@@ -921,7 +845,7 @@ static int jacobi(double *A, double *V, int b, int want_v)
                 if (g2 <= c2 * (alpha + beta) || g2 <= (JAC_TOL2 * alpha) * beta) continue;
                 rotated = 1;
                 double c, sn, tg;
-                rotation_any(alpha, beta, gamma, &c, &sn, &tg);
+                rotation(alpha, beta, gamma, &c, &sn, &tg);
                 nrm[i] = alpha - tg;
                 nrm[j] = beta + tg;
                 for (int r = 0; r < b; ++r) {

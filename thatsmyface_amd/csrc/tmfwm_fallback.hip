@@ -7,8 +7,8 @@
 // reconstruct, IDCT, inverse colour -- and overwrites their pixels.  extract_kernel<b>
 // appends the blocks whose sigma_1 enclosure does not decide f32(sigma_1) for either
 // image; extract_fixup_kernel<b> computes both sigma_1 on the dgesdd route and writes the
-// byte.  One thread per listed block; a grid-stride loop over the device-side count,
-// so no host round trip sits between the passes.
+// byte.  One thread per listed block, its working set in LDS; a grid-stride loop over the
+// device-side count, so no host round trip sits between the passes.
 #include "tmfwm_device.h"
 #include "tmfwm_internal.h"
 #include "tmfwm_lapack.h"
@@ -39,32 +39,65 @@ TMF_DEVI void load_dct_block(const uint8_t *frame, int W, int bi, int bj, float 
     for (int r = 0; r < B; ++r) dct::dct2<B>(y[r]);
 }
 
+// Each thread's dgesdd works in LDS, not in private (scratch) memory: A, U, VT, d, e, tauq,
+// taup and the work vectors (lp::ws_doubles), the block D and the f32 factors.  The route is
+// a serial chain of dependent loads and stores per block, so its latency is the memory's:
+// kFixT<B> threads per workgroup share <= 48 KB of LDS.
+template <int B>
+constexpr int kFixSlot = lp::ws_doubles(B) + (3 * B * B + B + 1) / 2;  // doubles per thread
+template <int B>
+constexpr int kFixT = (48 * 1024) / (8 * kFixSlot<B>) < 64 ? (48 * 1024) / (8 * kFixSlot<B>) : 64;
+template <int B>
+constexpr size_t kFixLds = (size_t)kFixT<B> * kFixSlot<B> * 8;
+
+struct FixSlot {
+    double *ws;
+    float *D, *U, *Vt, *S;
+};
+template <int B>
+TMF_DEVI FixSlot fix_slot(double *lds)
+{
+    FixSlot f;
+    f.ws = lds + threadIdx.x * kFixSlot<B>;
+    f.D = reinterpret_cast<float *>(f.ws + lp::ws_doubles(B));
+    f.U = f.D + B * B;
+    f.Vt = f.U + B * B;
+    f.S = f.Vt + B * B;
+    return f;
+}
+
 template <int B>
 __global__ __launch_bounds__(64) void embed_fixup_kernel(EmbedArgs a, const uint32_t *__restrict__ list, const uint32_t *__restrict__ count)
 {
+    extern __shared__ double fix_lds[];
+    constexpr int T = kFixT<B>;
+    const FixSlot f = fix_slot<B>(fix_lds);
     const uint32_t n = *count;
     const uint32_t per_frame = (uint32_t)a.nbh * (uint32_t)a.nbw;
-    for (uint32_t t = blockIdx.x * 64u + threadIdx.x; t < n; t += gridDim.x * 64u) {
+    for (uint32_t t = blockIdx.x * T + threadIdx.x; t < n; t += gridDim.x * T) {
         const uint32_t id = list[t];
-        const int64_t f = id / per_frame;
+        const int64_t fr = id / per_frame;
         const uint32_t rem = id % per_frame;
         const int bi = (int)(rem / (uint32_t)a.nbw), bj = (int)(rem % (uint32_t)a.nbw);
-        const uint8_t *src = a.src + f * a.frame_stride;
-        uint8_t *dst = a.dst + f * a.frame_stride;
+        const uint8_t *src = a.src + fr * a.frame_stride;
+        uint8_t *dst = a.dst + fr * a.frame_stride;
         float x[B][B];
         load_dct_block<B>(src, a.W, bi, bj, x);
-        float U[B * B], S[B], Vt[B * B];
-        lp::svd_f32<true>(&x[0][0], B, U, S, Vt);  // :195
+#pragma unroll
+        for (int i = 0; i < B; ++i)
+#pragma unroll
+            for (int j = 0; j < B; ++j) f.D[i * B + j] = x[i][j];
+        lp::svd_f32_ws<true>(f.D, B, f.U, f.S, f.Vt, f.ws);  // :195
         // :198 blend, :201 U @ (diag(S) @ Vt) as OpenBLAS sgemm's fma chain over k
         const double w = (double)a.wm[(int64_t)bi * a.nbw + bj];
-        S[0] = (float)((double)S[0] + a.alpha * (w / 255.0));
+        f.S[0] = (float)((double)f.S[0] + a.alpha * (w / 255.0));
 #pragma unroll
         for (int i = 0; i < B; ++i)
 #pragma unroll
             for (int j = 0; j < B; ++j) {
                 float acc = 0.0f;
 #pragma unroll
-                for (int k = 0; k < B; ++k) acc = __builtin_fmaf(U[i * B + k], S[k] * Vt[k * B + j], acc);
+                for (int k = 0; k < B; ++k) acc = __builtin_fmaf(f.U[i * B + k], f.S[k] * f.Vt[k * B + j], acc);
                 x[i][j] = acc;
             }
         // :204 IDCT, axis 0 then axis 1
@@ -99,27 +132,33 @@ __global__ __launch_bounds__(64) void embed_fixup_kernel(EmbedArgs a, const uint
 template <int B>
 __global__ __launch_bounds__(64) void extract_fixup_kernel(ExtractArgs a, const uint32_t *__restrict__ list, const uint32_t *__restrict__ count)
 {
+    extern __shared__ double fix_lds[];
+    constexpr int T = kFixT<B>;
+    const FixSlot f = fix_slot<B>(fix_lds);
     const uint32_t n = *count;
     const uint32_t per_frame = (uint32_t)a.nbh * (uint32_t)a.nbw;
-    for (uint32_t t = blockIdx.x * 64u + threadIdx.x; t < n; t += gridDim.x * 64u) {
+    for (uint32_t t = blockIdx.x * T + threadIdx.x; t < n; t += gridDim.x * T) {
         const uint32_t id = list[t];
-        const int64_t f = id / per_frame;
+        const int64_t fr = id / per_frame;
         const uint32_t rem = id % per_frame;
         const int bi = (int)(rem / (uint32_t)a.nbw), bj = (int)(rem % (uint32_t)a.nbw);
         float sig[2];
         for (int img = 0; img < 2; ++img) {
             float x[B][B];
-            load_dct_block<B>((img == 0 ? a.wsrc : a.osrc) + f * a.frame_stride, a.W, bi, bj, x);
-            float S[B];
-            lp::svd_f32<false>(&x[0][0], B, nullptr, S, nullptr);  // :279-282, S only
-            sig[img] = S[0];
+            load_dct_block<B>((img == 0 ? a.wsrc : a.osrc) + fr * a.frame_stride, a.W, bi, bj, x);
+#pragma unroll
+            for (int i = 0; i < B; ++i)
+#pragma unroll
+                for (int j = 0; j < B; ++j) f.D[i * B + j] = x[i][j];
+            lp::svd_f32_ws<false>(f.D, B, nullptr, f.S, nullptr, f.ws);  // :279-282, S only
+            sig[img] = f.S[0];
         }
         // :285-289 (numpy-2 NEP 50): f32 difference / f32(alpha); clip and *255 in f64; truncate
         const float e = (sig[0] - sig[1]) / a.alpha32;
         double d = (double)e;
         d = d < 0.0 ? 0.0 : d;
         d = d > 1.0 ? 1.0 : d;
-        a.out[f * a.tile_stride + (int64_t)bi * a.nbw + bj] = (uint8_t)(uint32_t)(d * 255.0);
+        a.out[fr * a.tile_stride + (int64_t)bi * a.nbw + bj] = (uint8_t)(uint32_t)(d * 255.0);
     }
 }
 
@@ -146,16 +185,17 @@ __global__ __launch_bounds__(64) void lp_nrm2_kernel(const double *__restrict__ 
 // launchers: the fixup grid is sized for the worst case (every block listed) but
 // capped; threads beyond the device-side count exit at once
 // ---------------------------------------------------------------------------
-static unsigned fixup_grid(int64_t max_entries)
+static unsigned fixup_grid(int64_t max_entries, int threads)
 {
-    const int64_t g = (max_entries + 63) / 64;
-    return (unsigned)(g < 1 ? 1 : (g > 4096 ? 4096 : g));
+    const int64_t g = (max_entries + threads - 1) / threads;
+    return (unsigned)(g < 1 ? 1 : (g > 8192 ? 8192 : g));
 }
 
 template <int B>
 static void embed_fixup_b(const EmbedArgs &a, const uint32_t *list, const uint32_t *count, int64_t max_entries, hipStream_t st)
 {
-    hipLaunchKernelGGL(embed_fixup_kernel<B>, dim3(fixup_grid(max_entries)), dim3(64), 0, st, a, list, count);
+    hipLaunchKernelGGL(embed_fixup_kernel<B>, dim3(fixup_grid(max_entries, kFixT<B>)), dim3(kFixT<B>), kFixLds<B>, st, a, list,
+                       count);
 }
 
 hipError_t launch_embed_fixup(const EmbedArgs &a, const uint32_t *list, const uint32_t *count, int64_t max_entries, hipStream_t st)
@@ -176,7 +216,8 @@ hipError_t launch_embed_fixup(const EmbedArgs &a, const uint32_t *list, const ui
 template <int B>
 static void extract_fixup_b(const ExtractArgs &a, const uint32_t *list, const uint32_t *count, int64_t max_entries, hipStream_t st)
 {
-    hipLaunchKernelGGL(extract_fixup_kernel<B>, dim3(fixup_grid(max_entries)), dim3(64), 0, st, a, list, count);
+    hipLaunchKernelGGL(extract_fixup_kernel<B>, dim3(fixup_grid(max_entries, kFixT<B>)), dim3(kFixT<B>), kFixLds<B>, st, a, list,
+                       count);
 }
 
 hipError_t launch_extract_fixup(const ExtractArgs &a, const uint32_t *list, const uint32_t *count, int64_t max_entries, hipStream_t st)

@@ -339,9 +339,8 @@ TMF_LPI int iladlr(int m, int n, const double *A, int lda)
     return r;
 }
 
-TMF_LPN void dlarf(int left, int m, int n, const double *v, int incv, double tau, double *C, int ldc)
+TMF_LPN void dlarf(int left, int m, int n, const double *v, int incv, double tau, double *C, int ldc, double *work)
 {
-    double work[kMaxN];
     int lastv = 0, lastc = 0;
     if (tau != 0.0) {
         lastv = left ? m : n;
@@ -359,20 +358,20 @@ TMF_LPN void dlarf(int left, int m, int n, const double *v, int incv, double tau
     }
 }
 
-TMF_LPN void dgebd2(int n, double *A, int lda, double *d, double *e, double *tauq, double *taup)
+TMF_LPN void dgebd2(int n, double *A, int lda, double *d, double *e, double *tauq, double *taup, double *work)
 {
     const int m = n;
     for (int i = 0; i < n; ++i) {
         dlarfg(m - i, &LP_AT(A, i, i, lda), &LP_AT(A, (i + 1 < m ? i + 1 : m - 1), i, lda), 1, &tauq[i]);
         d[i] = LP_AT(A, i, i, lda);
         LP_AT(A, i, i, lda) = 1.0;
-        if (i < n - 1) dlarf(1, m - i, n - i - 1, &LP_AT(A, i, i, lda), 1, tauq[i], &LP_AT(A, i, i + 1, lda), lda);
+        if (i < n - 1) dlarf(1, m - i, n - i - 1, &LP_AT(A, i, i, lda), 1, tauq[i], &LP_AT(A, i, i + 1, lda), lda, work);
         LP_AT(A, i, i, lda) = d[i];
         if (i < n - 1) {
             dlarfg(n - i - 1, &LP_AT(A, i, i + 1, lda), &LP_AT(A, i, (i + 2 < n ? i + 2 : n - 1), lda), lda, &taup[i]);
             e[i] = LP_AT(A, i, i + 1, lda);
             LP_AT(A, i, i + 1, lda) = 1.0;
-            dlarf(0, m - i - 1, n - i - 1, &LP_AT(A, i, i + 1, lda), lda, taup[i], &LP_AT(A, i + 1, i + 1, lda), lda);
+            dlarf(0, m - i - 1, n - i - 1, &LP_AT(A, i, i + 1, lda), lda, taup[i], &LP_AT(A, i + 1, i + 1, lda), lda, work);
             LP_AT(A, i, i + 1, lda) = e[i];
         } else {
             taup[i] = 0.0;
@@ -534,13 +533,12 @@ TMF_LPN void dlasr(bool left, bool fwd, int m, int n, const double *c, const dou
 // are those of the vector-carrying run -- not dlasq1's, which LAPACK would use without
 // vectors and numpy never does).  Returns 0, or 1 if not converged.
 template <bool WANT_V>
-TMF_LPN int dbdsqr(int n, double *d, double *e, double *VT, int ldvt, double *U, int ldu)
+TMF_LPN int dbdsqr(int n, double *d, double *e, double *VT, int ldvt, double *U, int ldu, double *work)
 {
     const int maxitr = 6;
     if (n == 0) return 0;
     if (n > 1) {
         const int nm1 = n - 1, nm12 = nm1 + nm1, nm13 = nm12 + nm1;
-        double work[4 * kMaxN];
         const double eps = kEps, unfl = kSafmin;
         const double tol = kTolmul * eps;
         double smax = 0.0;
@@ -780,7 +778,7 @@ TMF_LPN int dbdsqr(int n, double *d, double *e, double *VT, int ldvt, double *U,
 // dbdsdc('U', 'I') for n <= 25: U = VT = I, dlasdq -> dbdsqr, dlasdq's ascending
 // selection sort (.LT.), dbdsdc's descending selection sort (.GT.)
 template <bool WANT_V>
-TMF_LPN int dbdsdc(int n, double *d, double *e, double *U, int ldu, double *VT, int ldvt)
+TMF_LPN int dbdsdc(int n, double *d, double *e, double *U, int ldu, double *VT, int ldvt, double *work)
 {
     if (WANT_V)
         for (int j = 0; j < n; ++j)
@@ -790,7 +788,7 @@ TMF_LPN int dbdsdc(int n, double *d, double *e, double *U, int ldu, double *VT, 
         d[0] = __builtin_fabs(d[0]);
         return 0;
     }
-    const int info = dbdsqr<WANT_V>(n, d, e, VT, ldvt, U, ldu);
+    const int info = dbdsqr<WANT_V>(n, d, e, VT, ldvt, U, ldu, work);
     for (int i = 0; i < n; ++i) {
         int isub = i;
         double smin = d[i];
@@ -823,18 +821,18 @@ TMF_LPN int dbdsdc(int n, double *d, double *e, double *U, int ldu, double *VT, 
 }
 
 // dormbr('Q','L','N') -> dorm2r: H(k) ... H(1) applied backwards to U
-TMF_LPN void apply_q(int n, double *A, const double *tauq, double *U)
+TMF_LPN void apply_q(int n, double *A, const double *tauq, double *U, double *work)
 {
     for (int i = n - 1; i >= 0; --i) {
         const double aii = LP_AT(A, i, i, n);
         LP_AT(A, i, i, n) = 1.0;
-        dlarf(1, n - i, n, &LP_AT(A, i, i, n), 1, tauq[i], &LP_AT(U, i, 0, n), n);
+        dlarf(1, n - i, n, &LP_AT(A, i, i, n), 1, tauq[i], &LP_AT(U, i, 0, n), n, work);
         LP_AT(A, i, i, n) = aii;
     }
 }
 
 // dormbr('P','R','T'), nq = k = n -> dorml2('R','N', n, n-1, n-1, A(1,2), taup, VT(1,2))
-TMF_LPN void apply_pt(int n, double *A, const double *taup, double *VT)
+TMF_LPN void apply_pt(int n, double *A, const double *taup, double *VT, double *work)
 {
     if (n <= 1) return;
     double *A2 = A + n;
@@ -842,26 +840,31 @@ TMF_LPN void apply_pt(int n, double *A, const double *taup, double *VT)
     for (int i = n - 2; i >= 0; --i) {
         const double aii = A2[i + i * n];
         A2[i + i * n] = 1.0;
-        dlarf(0, n, n - 1 - i, &A2[i + i * n], n, taup[i], C2 + i * n, n);
+        dlarf(0, n, n - 1 - i, &A2[i + i * n], n, taup[i], C2 + i * n, n, work);
         A2[i + i * n] = aii;
     }
 }
 
+// Working set of one block's dgesdd: A, U, VT (n x n), d, e, tauq, taup (n), and the BLAS /
+// dbdsqr work vectors (n + 4n) -- in doubles.  The fixup kernels carve it out of LDS.
+TMF_LPI constexpr int ws_doubles(int n) { return 3 * n * n + 9 * n; }
+
 // np.linalg.svd of one float32 n x n block (row-major D): f32 U (row-major u[r][k]),
-// S, Vt (row-major vt[k][j]) exactly as numpy returns them.  Returns dbdsqr's info.
+// S, Vt (row-major vt[k][j]) exactly as numpy returns them, in the caller's workspace
+// ws (ws_doubles(n)).  Returns dbdsqr's info.
 template <bool WANT_V>
-TMF_LPN int svd_f32(const float *D, int n, float *Uo, float *So, float *Vto)
+TMF_LPN int svd_f32_ws(const float *D, int n, float *Uo, float *So, float *Vto, double *ws)
 {
-    double A[kMaxN * kMaxN], U[kMaxN * kMaxN], VT[kMaxN * kMaxN];
-    double d[kMaxN], e[kMaxN], tauq[kMaxN], taup[kMaxN];
+    double *A = ws, *U = A + n * n, *VT = U + n * n, *d = VT + n * n, *e = d + n, *tauq = e + n, *taup = tauq + n,
+           *work = taup + n;
     for (int i = 0; i < n; ++i)
         for (int j = 0; j < n; ++j) A[i + j * n] = (double)D[i * n + j];
     // dgesdd scales only when max|a| is outside [sqrt(safmin)/prec, its inverse]: never for f32 data
-    dgebd2(n, A, n, d, e, tauq, taup);
-    const int info = dbdsdc<WANT_V>(n, d, e, U, n, VT, n);
+    dgebd2(n, A, n, d, e, tauq, taup, work);
+    const int info = dbdsdc<WANT_V>(n, d, e, U, n, VT, n, work);
     if (WANT_V) {
-        apply_q(n, A, tauq, U);
-        apply_pt(n, A, taup, VT);
+        apply_q(n, A, tauq, U, work);
+        apply_pt(n, A, taup, VT, work);
         for (int i = 0; i < n; ++i)
             for (int k = 0; k < n; ++k) {
                 Uo[i * n + k] = (float)U[i + k * n];
@@ -870,6 +873,14 @@ TMF_LPN int svd_f32(const float *D, int n, float *Uo, float *So, float *Vto)
     }
     for (int k = 0; k < n; ++k) So[k] = (float)d[k];
     return info;
+}
+
+// the same with a private workspace (stage entry point, host builds)
+template <bool WANT_V>
+TMF_LPN int svd_f32(const float *D, int n, float *Uo, float *So, float *Vto)
+{
+    double ws[ws_doubles(kMaxN)];
+    return svd_f32_ws<WANT_V>(D, n, Uo, So, Vto, ws);
 }
 
 }  // namespace lp
