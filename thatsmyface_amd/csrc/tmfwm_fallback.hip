@@ -1,164 +1,56 @@
-// The dgesdd route on the GPU (tmfwm_lapack.h): the second pass of embed and extract,
-// plus the stage entry points the parity tests call.
-//
-// embed_kernel<b> runs the Jacobi route on every block and appends to a list the blocks
-// whose conditioning test fails; embed_fixup_kernel<b> redoes exactly
-// those blocks end to end -- luma, DCT, np.linalg.svd as LAPACK computes it, blend,
-// reconstruct, IDCT, inverse colour -- and overwrites their pixels.  extract_kernel<b>
-// appends the blocks whose sigma_1 enclosure does not decide f32(sigma_1) for either
-// image; extract_fixup_kernel<b> computes both sigma_1 on the dgesdd route and writes the
-// byte.  One thread per listed block, its working set in LDS; a grid-stride loop over the
-// device-side count, so no host round trip sits between the passes.
-#include "tmfwm_device.h"
-#include "tmfwm_internal.h"
-#include "tmfwm_lapack.h"
+// The dgesdd route on the GPU: dispatch of the second passes (tmfwm_fixup.h, one TU per block
+// size: tmfwm_fixup<b>.hip) and the stage entry points the parity tests call.
+#include "tmfwm_fixup.h"
 
 namespace tmf {
 
-template <int B>
-TMF_DEVI void load_dct_block(const uint8_t *frame, int W, int bi, int bj, float (&y)[B][B])
+hipStream_t aux_stream()
 {
-#pragma unroll
-    for (int r = 0; r < B; ++r)
-#pragma unroll
-        for (int c = 0; c < B; ++c) {
-            const uint8_t *p = frame + ((int64_t)(bi * B + r) * W + (int64_t)bj * B + c) * 3;
-            y[r][c] = luma(p[0], p[1], p[2]);
-        }
-    // :192 / :279-282 -- DCT along axis 0, then axis 1
-#pragma unroll
-    for (int c = 0; c < B; ++c) {
-        float col[B];
-#pragma unroll
-        for (int r = 0; r < B; ++r) col[r] = y[r][c];
-        dct::dct2<B>(col);
-#pragma unroll
-        for (int r = 0; r < B; ++r) y[r][c] = col[r];
-    }
-#pragma unroll
-    for (int r = 0; r < B; ++r) dct::dct2<B>(y[r]);
+    static std::mutex mu;
+    static hipStream_t streams[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    std::lock_guard<std::mutex> lk(mu);
+    if (!streams[dev] && hipStreamCreateWithFlags(&streams[dev], hipStreamNonBlocking) != hipSuccess) streams[dev] = nullptr;
+    return streams[dev];
 }
 
-// Each thread's dgesdd works in LDS, not in private (scratch) memory: A, U, VT, d, e, tauq,
-// taup and the work vectors (lp::ws_doubles), the block D and the f32 factors.  The route is
-// a serial chain of dependent loads and stores per block, so its latency is the memory's:
-// kFixT<B> threads per workgroup share <= 48 KB of LDS.
-template <int B>
-constexpr int kFixSlot = lp::ws_doubles(B) + (3 * B * B + B + 1) / 2;  // doubles per thread
-template <int B>
-constexpr int kFixT = (48 * 1024) / (8 * kFixSlot<B>) < 64 ? (48 * 1024) / (8 * kFixSlot<B>) : 64;
-template <int B>
-constexpr size_t kFixLds = (size_t)kFixT<B> * kFixSlot<B> * 8;
+#define TMF_FIXUP_DECL(B)                                                                                                    \
+    hipError_t launch_embed_fixup_##B(const EmbedArgs &, const uint32_t *, const uint32_t *, int64_t, hipStream_t);          \
+    hipError_t launch_extract_fixup_##B(const ExtractArgs &, const uint32_t *, const uint32_t *, int64_t, hipStream_t);
+TMF_FIXUP_DECL(4)
+TMF_FIXUP_DECL(6)
+TMF_FIXUP_DECL(8)
+TMF_FIXUP_DECL(10)
+TMF_FIXUP_DECL(12)
+TMF_FIXUP_DECL(14)
+TMF_FIXUP_DECL(16)
 
-struct FixSlot {
-    double *ws;
-    float *D, *U, *Vt, *S;
-};
-template <int B>
-TMF_DEVI FixSlot fix_slot(double *lds)
+hipError_t launch_embed_fixup(const EmbedArgs &a, const uint32_t *list, const uint32_t *count, int64_t max_entries, hipStream_t st)
 {
-    FixSlot f;
-    f.ws = lds + threadIdx.x * kFixSlot<B>;
-    f.D = reinterpret_cast<float *>(f.ws + lp::ws_doubles(B));
-    f.U = f.D + B * B;
-    f.Vt = f.U + B * B;
-    f.S = f.Vt + B * B;
-    return f;
-}
-
-template <int B>
-__global__ __launch_bounds__(64) void embed_fixup_kernel(EmbedArgs a, const uint32_t *__restrict__ list, const uint32_t *__restrict__ count)
-{
-    extern __shared__ double fix_lds[];
-    constexpr int T = kFixT<B>;
-    const FixSlot f = fix_slot<B>(fix_lds);
-    const uint32_t n = *count;
-    const uint32_t per_frame = (uint32_t)a.nbh * (uint32_t)a.nbw;
-    for (uint32_t t = blockIdx.x * T + threadIdx.x; t < n; t += gridDim.x * T) {
-        const uint32_t id = list[t];
-        const int64_t fr = id / per_frame;
-        const uint32_t rem = id % per_frame;
-        const int bi = (int)(rem / (uint32_t)a.nbw), bj = (int)(rem % (uint32_t)a.nbw);
-        const uint8_t *src = a.src + fr * a.frame_stride;
-        uint8_t *dst = a.dst + fr * a.frame_stride;
-        float x[B][B];
-        load_dct_block<B>(src, a.W, bi, bj, x);
-#pragma unroll
-        for (int i = 0; i < B; ++i)
-#pragma unroll
-            for (int j = 0; j < B; ++j) f.D[i * B + j] = x[i][j];
-        lp::svd_f32_ws<true>(f.D, B, f.U, f.S, f.Vt, f.ws);  // :195
-        // :198 blend, :201 U @ (diag(S) @ Vt) as OpenBLAS sgemm's fma chain over k
-        const double w = (double)a.wm[(int64_t)bi * a.nbw + bj];
-        f.S[0] = (float)((double)f.S[0] + a.alpha * (w / 255.0));
-#pragma unroll
-        for (int i = 0; i < B; ++i)
-#pragma unroll
-            for (int j = 0; j < B; ++j) {
-                float acc = 0.0f;
-#pragma unroll
-                for (int k = 0; k < B; ++k) acc = __builtin_fmaf(f.U[i * B + k], f.S[k] * f.Vt[k * B + j], acc);
-                x[i][j] = acc;
-            }
-        // :204 IDCT, axis 0 then axis 1
-#pragma unroll
-        for (int c = 0; c < B; ++c) {
-            float col[B];
-#pragma unroll
-            for (int r = 0; r < B; ++r) col[r] = x[r][c];
-            dct::dct3<B>(col);
-#pragma unroll
-            for (int r = 0; r < B; ++r) x[r][c] = col[r];
-        }
-#pragma unroll
-        for (int r = 0; r < B; ++r) dct::dct3<B>(x[r]);
-        // :207-216 write back with the pixel's own chroma, inverse colour
-#pragma unroll
-        for (int r = 0; r < B; ++r)
-#pragma unroll
-            for (int c = 0; c < B; ++c) {
-                const int64_t off = ((int64_t)(bi * B + r) * a.W + (int64_t)bj * B + c) * 3;
-                float cbs, crs;
-                chroma(src[off], src[off + 1], src[off + 2], cbs, crs);
-                uint32_t R8, G8, B8;
-                colour_inv(x[r][c], cbs, crs, R8, G8, B8);
-                dst[off] = (uint8_t)R8;
-                dst[off + 1] = (uint8_t)G8;
-                dst[off + 2] = (uint8_t)B8;
-            }
+    switch (a.block) {
+    case 4: return launch_embed_fixup_4(a, list, count, max_entries, st);
+    case 6: return launch_embed_fixup_6(a, list, count, max_entries, st);
+    case 8: return launch_embed_fixup_8(a, list, count, max_entries, st);
+    case 10: return launch_embed_fixup_10(a, list, count, max_entries, st);
+    case 12: return launch_embed_fixup_12(a, list, count, max_entries, st);
+    case 14: return launch_embed_fixup_14(a, list, count, max_entries, st);
+    case 16: return launch_embed_fixup_16(a, list, count, max_entries, st);
+    default: return hipErrorInvalidValue;
     }
 }
 
-template <int B>
-__global__ __launch_bounds__(64) void extract_fixup_kernel(ExtractArgs a, const uint32_t *__restrict__ list, const uint32_t *__restrict__ count)
+hipError_t launch_extract_fixup(const ExtractArgs &a, const uint32_t *list, const uint32_t *count, int64_t max_entries, hipStream_t st)
 {
-    extern __shared__ double fix_lds[];
-    constexpr int T = kFixT<B>;
-    const FixSlot f = fix_slot<B>(fix_lds);
-    const uint32_t n = *count;
-    const uint32_t per_frame = (uint32_t)a.nbh * (uint32_t)a.nbw;
-    for (uint32_t t = blockIdx.x * T + threadIdx.x; t < n; t += gridDim.x * T) {
-        const uint32_t id = list[t];
-        const int64_t fr = id / per_frame;
-        const uint32_t rem = id % per_frame;
-        const int bi = (int)(rem / (uint32_t)a.nbw), bj = (int)(rem % (uint32_t)a.nbw);
-        float sig[2];
-        for (int img = 0; img < 2; ++img) {
-            float x[B][B];
-            load_dct_block<B>((img == 0 ? a.wsrc : a.osrc) + fr * a.frame_stride, a.W, bi, bj, x);
-#pragma unroll
-            for (int i = 0; i < B; ++i)
-#pragma unroll
-                for (int j = 0; j < B; ++j) f.D[i * B + j] = x[i][j];
-            lp::svd_f32_ws<false>(f.D, B, nullptr, f.S, nullptr, f.ws);  // :279-282, S only
-            sig[img] = f.S[0];
-        }
-        // :285-289 (numpy-2 NEP 50): f32 difference / f32(alpha); clip and *255 in f64; truncate
-        const float e = (sig[0] - sig[1]) / a.alpha32;
-        double d = (double)e;
-        d = d < 0.0 ? 0.0 : d;
-        d = d > 1.0 ? 1.0 : d;
-        a.out[fr * a.tile_stride + (int64_t)bi * a.nbw + bj] = (uint8_t)(uint32_t)(d * 255.0);
+    switch (a.block) {
+    case 4: return launch_extract_fixup_4(a, list, count, max_entries, st);
+    case 6: return launch_extract_fixup_6(a, list, count, max_entries, st);
+    case 8: return launch_extract_fixup_8(a, list, count, max_entries, st);
+    case 10: return launch_extract_fixup_10(a, list, count, max_entries, st);
+    case 12: return launch_extract_fixup_12(a, list, count, max_entries, st);
+    case 14: return launch_extract_fixup_14(a, list, count, max_entries, st);
+    case 16: return launch_extract_fixup_16(a, list, count, max_entries, st);
+    default: return hipErrorInvalidValue;
     }
 }
 
@@ -179,60 +71,6 @@ __global__ __launch_bounds__(64) void lp_nrm2_kernel(const double *__restrict__ 
 {
     const int64_t k = (int64_t)blockIdx.x * 64 + threadIdx.x;
     if (k < nvec) out[k] = lp::dnrm2(n, x + k * (int64_t)n * inc, inc);
-}
-
-// ---------------------------------------------------------------------------
-// launchers: the fixup grid is sized for the worst case (every block listed) but
-// capped; threads beyond the device-side count exit at once
-// ---------------------------------------------------------------------------
-static unsigned fixup_grid(int64_t max_entries, int threads)
-{
-    const int64_t g = (max_entries + threads - 1) / threads;
-    return (unsigned)(g < 1 ? 1 : (g > 8192 ? 8192 : g));
-}
-
-template <int B>
-static void embed_fixup_b(const EmbedArgs &a, const uint32_t *list, const uint32_t *count, int64_t max_entries, hipStream_t st)
-{
-    hipLaunchKernelGGL(embed_fixup_kernel<B>, dim3(fixup_grid(max_entries, kFixT<B>)), dim3(kFixT<B>), kFixLds<B>, st, a, list,
-                       count);
-}
-
-hipError_t launch_embed_fixup(const EmbedArgs &a, const uint32_t *list, const uint32_t *count, int64_t max_entries, hipStream_t st)
-{
-    switch (a.block) {
-    case 4: embed_fixup_b<4>(a, list, count, max_entries, st); break;
-    case 6: embed_fixup_b<6>(a, list, count, max_entries, st); break;
-    case 8: embed_fixup_b<8>(a, list, count, max_entries, st); break;
-    case 10: embed_fixup_b<10>(a, list, count, max_entries, st); break;
-    case 12: embed_fixup_b<12>(a, list, count, max_entries, st); break;
-    case 14: embed_fixup_b<14>(a, list, count, max_entries, st); break;
-    case 16: embed_fixup_b<16>(a, list, count, max_entries, st); break;
-    default: return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
-}
-
-template <int B>
-static void extract_fixup_b(const ExtractArgs &a, const uint32_t *list, const uint32_t *count, int64_t max_entries, hipStream_t st)
-{
-    hipLaunchKernelGGL(extract_fixup_kernel<B>, dim3(fixup_grid(max_entries, kFixT<B>)), dim3(kFixT<B>), kFixLds<B>, st, a, list,
-                       count);
-}
-
-hipError_t launch_extract_fixup(const ExtractArgs &a, const uint32_t *list, const uint32_t *count, int64_t max_entries, hipStream_t st)
-{
-    switch (a.block) {
-    case 4: extract_fixup_b<4>(a, list, count, max_entries, st); break;
-    case 6: extract_fixup_b<6>(a, list, count, max_entries, st); break;
-    case 8: extract_fixup_b<8>(a, list, count, max_entries, st); break;
-    case 10: extract_fixup_b<10>(a, list, count, max_entries, st); break;
-    case 12: extract_fixup_b<12>(a, list, count, max_entries, st); break;
-    case 14: extract_fixup_b<14>(a, list, count, max_entries, st); break;
-    case 16: extract_fixup_b<16>(a, list, count, max_entries, st); break;
-    default: return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
 }
 
 hipError_t launch_lapack_svd_blocks(const float *D, int64_t nb, int block, float *U, float *S, float *Vt, int want_v, int32_t *info,

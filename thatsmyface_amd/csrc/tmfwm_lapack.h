@@ -27,7 +27,7 @@ namespace lp {
 // host + device: the CPU test suite compiles this same code for the host
 // (tests/native/lp_host.cpp) and checks it against the oracle before any GPU run
 #define TMF_LPI __host__ __device__ inline __attribute__((always_inline))
-#define TMF_LPN __host__ __device__ __attribute__((noinline))
+#define TMF_LPN __host__ __device__ inline __attribute__((noinline))  // inline: one definition per TU is fine (tmfwm_fixup<b>.hip)
 
 constexpr int kMaxN = 16;
 constexpr double kEps = 0x1p-53;                     // dlamch('E')

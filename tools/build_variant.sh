@@ -1,8 +1,9 @@
 #!/bin/bash
 # Build an experimental library variant: tools/build_variant.sh <name> [extra hipcc flags...]
 # -> variants/libtmfwm_<name>.so (git-ignored; travels to the GPU box; load it with TMFWM_LIB).
-# Only the kernel TUs take the extra flags; the ABI / tile / dgesdd-route objects are the
-# main build's (make -C thatsmyface_amd/csrc first).
+# The kernel TUs take the extra flags; with FALLBACK=1 in the environment the dgesdd-route
+# TU (tmfwm_fallback.hip) is recompiled with them too, otherwise the ABI / tile / QR /
+# dgesdd-route objects are the main build's (make -C thatsmyface_amd/csrc first).
 set -euo pipefail
 NAME=$1; shift
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
@@ -12,9 +13,18 @@ T=$(mktemp -d)
 F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -fno-slp-vectorize -Wall $*"
 /opt/rocm/bin/hipcc $F -c "$C/tmfwm_kernels.hip" -o "$T/k.o" &
 /opt/rocm/bin/hipcc $F -mllvm -amdgpu-sched-strategy=max-ilp -c "$C/tmfwm_embed8.hip" -o "$T/e8.o" &
+FB="$C/tmfwm_fallback.o $C/tmfwm_fixup4.o $C/tmfwm_fixup6.o $C/tmfwm_fixup8.o $C/tmfwm_fixup10.o $C/tmfwm_fixup12.o $C/tmfwm_fixup14.o $C/tmfwm_fixup16.o"
+if [ "${FALLBACK:-0}" = "1" ]; then
+  FB="$T/fb.o"
+  /opt/rocm/bin/hipcc $F -c "$C/tmfwm_fallback.hip" -o "$T/fb.o" &
+  for b in 4 6 8 10 12 14 16; do
+    /opt/rocm/bin/hipcc $F -c "$C/tmfwm_fixup$b.hip" -o "$T/fx$b.o" &
+    FB="$FB $T/fx$b.o"
+  done
+fi
 wait
 mkdir -p "$ROOT/variants"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$ROOT/variants/libtmfwm_$NAME.so" "$T/k.o" "$T/e8.o" \
-    "$C/tmfwm_capi.o" "$C/tmfwm_multi.o" "$C/tmfwm_qr.o" "$C/tmfwm_tile.o" "$C/tmfwm_fallback.o" -fopenmp -ldl -lpthread
+    "$C/tmfwm_capi.o" "$C/tmfwm_multi.o" "$C/tmfwm_qr.o" "$C/tmfwm_tile.o" $FB -fopenmp -ldl -lpthread
 rm -rf "$T"
 echo "variants/libtmfwm_$NAME.so"
