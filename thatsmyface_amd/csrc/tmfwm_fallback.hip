@@ -2,6 +2,8 @@
 // size: tmfwm_fixup<b>.hip) and the stage entry points the parity tests call.
 #include "tmfwm_fixup.h"
 
+#include <cstdlib>
+
 namespace tmf {
 
 hipStream_t aux_stream()
@@ -13,6 +15,15 @@ hipStream_t aux_stream()
     std::lock_guard<std::mutex> lk(mu);
     if (!streams[dev] && hipStreamCreateWithFlags(&streams[dev], hipStreamNonBlocking) != hipSuccess) streams[dev] = nullptr;
     return streams[dev];
+}
+
+bool fixup_lead_disabled()
+{
+    static const bool off = [] {
+        const char *e = std::getenv("TMFWM_DEBUG_NO_LEAD");
+        return e && *e && *e != '0';
+    }();
+    return off;
 }
 
 #define TMF_FIXUP_DECL(B)                                                                                                    \

@@ -47,6 +47,17 @@ TMF_DEVI void load_dct_block(const uint8_t *frame, int W, int bi, int bj, float 
 // taup and the work vectors (lp::ws_doubles), the block D and the f32 factors.  The route is
 // a serial chain of dependent loads and stores per block, so its latency is the memory's:
 // kFixT<B> threads per workgroup share <= 48 KB of LDS.
+// The block size reaches the dgesdd routines as a run-time value, as it does from the stage
+// kernel (lp_svd_blocks_kernel): with every call site in a TU passing the constant B, the
+// compiler specialises the noinline routines on it (a TU per block size, tmfwm_fixup<b>.hip),
+// and the b = 16 specialisation faulted on the GPU (illegal address) where the shared,
+// run-time-n code -- host-sanitiser clean, GPU parity green -- does not.
+TMF_DEVI int runtime_n(int n)
+{
+    asm volatile("" : "+v"(n));
+    return n;
+}
+
 template <int B>
 constexpr int kFixSlot = lp::ws_doubles(B) + (3 * B * B + B + 1) / 2;  // doubles per thread
 // Two launches share the list (launch_fixup below).  The route's control flow depends on the
@@ -100,7 +111,7 @@ __global__ __launch_bounds__(64) void embed_fixup_kernel(EmbedArgs a, const uint
         for (int i = 0; i < B; ++i)
 #pragma unroll
             for (int j = 0; j < B; ++j) f.D[i * B + j] = x[i][j];
-        lp::svd_f32_ws<true>(f.D, B, f.U, f.S, f.Vt, f.ws);  // :195
+        lp::svd_f32_ws<true>(f.D, runtime_n(B), f.U, f.S, f.Vt, f.ws);  // :195
         // :198 blend, :201 U @ (diag(S) @ Vt) as OpenBLAS sgemm's fma chain over k
         const double w = (double)a.wm[(int64_t)bi * a.nbw + bj];
         f.S[0] = (float)((double)f.S[0] + a.alpha * (w / 255.0));
@@ -163,7 +174,7 @@ __global__ __launch_bounds__(64) void extract_fixup_kernel(ExtractArgs a, const 
             for (int i = 0; i < B; ++i)
 #pragma unroll
                 for (int j = 0; j < B; ++j) f.D[i * B + j] = x[i][j];
-            lp::svd_f32_ws<false>(f.D, B, nullptr, f.S, nullptr, f.ws);  // :279-282, S only
+            lp::svd_f32_ws<false>(f.D, runtime_n(B), nullptr, f.S, nullptr, f.ws);  // :279-282, S only
             sig[img] = f.S[0];
         }
         // :285-289 (numpy-2 NEP 50): f32 difference / f32(alpha); clip and *255 in f64; truncate
@@ -191,9 +202,15 @@ hipStream_t aux_stream();  // tmfwm_fallback.hip
 
 // lead launch on st for entries [0, kLead); if the list can be longer, the bulk launch for
 // [kLead, count) on the auxiliary stream, forked from and joined back into st
+bool fixup_lead_disabled();  // TMFWM_DEBUG_NO_LEAD (tmfwm_fallback.hip): every entry to the bulk launch
+
 template <typename Lead, typename Bulk>
 inline hipError_t launch_fixup(int64_t max_entries, hipStream_t st, Lead lead, Bulk bulk)
 {
+    if (fixup_lead_disabled()) {
+        bulk(st, 0u);
+        return hipGetLastError();
+    }
     if (max_entries <= (int64_t)kLead) {
         lead(st);
         return hipGetLastError();
@@ -205,7 +222,7 @@ inline hipError_t launch_fixup(int64_t max_entries, hipStream_t st, Lead lead, B
     if (e == hipSuccess) e = hipEventRecord(fork, st);
     if (e == hipSuccess) e = hipStreamWaitEvent(aux, fork, 0);
     if (e == hipSuccess) {
-        bulk(aux);
+        bulk(aux, kLead);
         e = hipGetLastError();
     }
     if (e == hipSuccess) e = hipEventRecord(join, aux);
@@ -229,9 +246,9 @@ inline hipError_t embed_fixup_b(const EmbedArgs &a, const uint32_t *list, const 
             hipLaunchKernelGGL((embed_fixup_kernel<B, 1>), dim3(fixup_grid(max_entries < kLead ? max_entries : kLead, 1)), dim3(1),
                                kFixSlot<B> * 8, s, a, list, count, 0u, kLead);
         },
-        [&](hipStream_t s) {
-            hipLaunchKernelGGL((embed_fixup_kernel<B, T>), dim3(fixup_grid(max_entries - kLead, T)), dim3(T), (size_t)T * kFixSlot<B> * 8,
-                               s, a, list, count, kLead, 0xFFFFFFFFu);
+        [&](hipStream_t s, uint32_t lo) {
+            hipLaunchKernelGGL((embed_fixup_kernel<B, T>), dim3(fixup_grid(max_entries - lo, T)), dim3(T), (size_t)T * kFixSlot<B> * 8, s,
+                               a, list, count, lo, 0xFFFFFFFFu);
         });
 }
 
@@ -245,9 +262,9 @@ inline hipError_t extract_fixup_b(const ExtractArgs &a, const uint32_t *list, co
             hipLaunchKernelGGL((extract_fixup_kernel<B, 1>), dim3(fixup_grid(max_entries < kLead ? max_entries : kLead, 1)), dim3(1),
                                kFixSlot<B> * 8, s, a, list, count, 0u, kLead);
         },
-        [&](hipStream_t s) {
-            hipLaunchKernelGGL((extract_fixup_kernel<B, T>), dim3(fixup_grid(max_entries - kLead, T)), dim3(T),
-                               (size_t)T * kFixSlot<B> * 8, s, a, list, count, kLead, 0xFFFFFFFFu);
+        [&](hipStream_t s, uint32_t lo) {
+            hipLaunchKernelGGL((extract_fixup_kernel<B, T>), dim3(fixup_grid(max_entries - lo, T)), dim3(T), (size_t)T * kFixSlot<B> * 8,
+                               s, a, list, count, lo, 0xFFFFFFFFu);
         });
 }
 
