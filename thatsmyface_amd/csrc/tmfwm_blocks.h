@@ -193,7 +193,7 @@ template <int B>
 __global__ __launch_bounds__(64, kEmbedWaves<B>) void embed_kernel(EmbedArgs a)
 {
     constexpr int L = Geo<B>::L, R = Geo<B>::R, BPW = Geo<B>::BPW, LD = B + 1, NW = Geo<B>::NW;
-    __shared__ float lds[BPW * B * LD];
+    __shared__ __attribute__((aligned(16))) float lds[BPW * B * LD];  // also the column norms during the SVD
     __shared__ uint32_t pix[R * NW][64];  // this lane's source bytes, parked during the SVD
     const int lane = threadIdx.x & 63, g = lane / L, q = lane % L;
     float *tile = lds + g * B * LD;
@@ -216,7 +216,7 @@ __global__ __launch_bounds__(64, kEmbedWaves<B>) void embed_kernel(EmbedArgs a)
     stamp(0);
 
     double A[R][B], V[R][B];
-    svd3<B, L>(x, A, V, q, stamp);  // :195 (SVD)
+    svd3<B, L>(x, A, V, q, stamp, tile);  // :195 (SVD); norms in the block's tile (kLdsNorms)
 
     // singular values, U = A / sigma, sort descending (oracle orc_svd_block)
     double sig[B];

@@ -858,13 +858,48 @@ TMF_DEVI Rot<T> rotation(T alpha, T beta, T gamma)
 template <int B, int L>
 constexpr int kRows = (B + L - 1) / L;
 
+// Norms in LDS (8-lane blocks, b = 14 / 16, one pair per lane): instead of every lane
+// holding all b column norms, selecting its pair's two by lane-masked blends and applying
+// every pair's t*gamma, the block keeps one copy of the norms in LDS (written once per
+// sweep by the block's first lane); the owner of a pair reads its two norms there and,
+// when it rotates, writes them back updated.  Same operations on the same values as the
+// register form, so the same bits; 32 fewer live VGPRs (the norms) in the f64 phase,
+// ~40 fewer VALU operations and 16 fewer broadcasts (t*gamma) per round.
+#ifndef TMF_LDS_NORMS
+#define TMF_LDS_NORMS 1
+#endif
+#ifndef TMF_LN_MIN_L  // smallest block group that keeps its norms in LDS (timing experiments)
+#define TMF_LN_MIN_L 8
+#endif
+template <int L>
+constexpr bool kLdsNorms = TMF_LDS_NORMS && L >= 2 && L >= TMF_LN_MIN_L;
+#ifndef TMF_LN_TYPES  // which phases keep their norms in LDS (timing experiments: tools/build_variant.sh)
+#define TMF_LN_TYPES(T) (std::is_same_v<T, double>)
+#endif
+
+// pair p's lower / higher column for every p < b/2 of round s, one 4-bit field per lane
+// p; a lane without a pair (p >= b/2: b = 14) gets slot 15, a dummy past the b norms
+template <int B, int S, bool HI>
+constexpr uint32_t sched_nibbles()
+{
+    uint32_t v = 0;
+    for (int p = 0; p < 8; ++p) v |= (uint32_t)(p < B / 2 ? (HI ? Sched<B>::hi(S, p) : Sched<B>::lo(S, p)) : 15) << (4 * p);
+    return v;
+}
+
+// keeps the compiler from moving this block's LDS norm accesses across a round boundary
+// (the lanes of a wave see each other's LDS writes in program order)
+TMF_DEVI void lds_order() { asm volatile("" ::: "memory"); }
+
 template <typename T, int B, int L, bool WANT_V>
-TMF_DEVI int jacobi(T (&A)[(B + L - 1) / L][B], T (&V)[(B + L - 1) / L][B], int q)
+TMF_DEVI int jacobi(T (&A)[(B + L - 1) / L][B], T (&V)[(B + L - 1) / L][B], int q, T *nl = nullptr)
 {
     using P = JacP<T>;
     // NP pairs per round; lane q evaluates pairs [q*PP, q*PP + PP) that exist
     constexpr int R = kRows<B, L>, NP = B / 2, PP = (NP + L - 1) / L;
     constexpr bool kBranchy = P::kBranchy;
+    constexpr bool kLN = kLdsNorms<L> && TMF_LN_TYPES(T);
+    static_assert(!kLN || NP <= 8, "LDS norms: 4-bit pair table");
     T F = T(0);
     static_for<B>([&](auto K) { F += cdot<R, B, L>(A, K, K); });
     const T c2 = P::kC2 * F;
@@ -882,6 +917,11 @@ TMF_DEVI int jacobi(T (&A)[(B + L - 1) / L][B], T (&V)[(B + L - 1) / L][B], int 
         // so that the chains interleave and no DPP read waits on the write just before it
         static_for<B>([&](auto K) { nrm[K] = cdot_part<R, B>(A, K, K); });
         static_for<B>([&](auto K) { nrm[K] = group_sum<L>(nrm[K]); });
+        if constexpr (kLN) {
+            lds_order();
+            if (q == 0) static_for<B>([&](auto K) { nl[K] = nrm[K]; });
+            lds_order();
+        }
         int rotated = 0;  // this lane rotated one of its own pairs this sweep
         static_for<B - 1>([&](auto S) {
             constexpr int s = S;
@@ -895,9 +935,20 @@ TMF_DEVI int jacobi(T (&A)[(B + L - 1) / L][B], T (&V)[(B + L - 1) / L][B], int 
             // (only here -- the owner's flag travels with its parameters), rotation
             Rot<T> mine[PP];
             unsigned long long own_ball[PP];  // wave mask of the lanes whose U-th pair rotates
+            int own_i = 0, own_j = 0;  // kLN: this lane's pair's columns
             static_for<PP>([&](auto U) {
                 constexpr int p0 = U, i0 = Sched<B>::lo(s, p0), j0 = Sched<B>::hi(s, p0);
-                T a = nrm[i0], b = nrm[j0], g = ga[p0];
+                T a, b, g = ga[p0];
+                if constexpr (kLN) {
+                    const int pq = q * PP + p0;  // this lane's U-th pair
+                    own_i = (int)__builtin_amdgcn_ubfe(sched_nibbles<B, s, false>(), 4 * pq, 4);
+                    own_j = (int)__builtin_amdgcn_ubfe(sched_nibbles<B, s, true>(), 4 * pq, 4);
+                    a = nl[own_i];
+                    b = nl[own_j];
+                } else {
+                    a = nrm[i0];
+                    b = nrm[j0];
+                }
                 int slot = -1;  // lane has a U-th pair this round
                 static_for<L - 1>([&](auto Q1) {
                     constexpr int QQ = Q1 + 1, p = QQ * PP + U;
@@ -905,8 +956,10 @@ TMF_DEVI int jacobi(T (&A)[(B + L - 1) / L][B], T (&V)[(B + L - 1) / L][B], int 
                     asm volatile("" : "+v"(m));
                     if constexpr (p < NP) {
                         constexpr int i = Sched<B>::lo(s, p), j = Sched<B>::hi(s, p);
-                        a = blend(m, nrm[i], a);
-                        b = blend(m, nrm[j], b);
+                        if constexpr (!kLN) {
+                            a = blend(m, nrm[i], a);
+                            b = blend(m, nrm[j], b);
+                        }
                         g = blend(m, ga[p], g);
                     } else {
                         slot &= ~m;
@@ -925,20 +978,26 @@ TMF_DEVI int jacobi(T (&A)[(B + L - 1) / L][B], T (&V)[(B + L - 1) / L][B], int 
                     mine[U].s = o ? r.s : T(0);
                     mine[U].tg = o ? r.tg : T(0);
                 }
+                if constexpr (kLN) {  // every lane writes its pair's norms back: old value -+ t*gamma
+                    nl[own_i] = a - mine[U].tg;  // (t*gamma = 0 when it does not rotate: the same bits)
+                    nl[own_j] = b + mine[U].tg;
+                }
             });
             static_for<NP>([&](auto Pi) {
                 constexpr int p = Pi, i = Sched<B>::lo(s, p), j = Sched<B>::hi(s, p), u = p % PP, src = p / PP;
                 const T c = group_bcast<L, src>(mine[u].c);
                 const T sn = group_bcast<L, src>(mine[u].s);
-                const T tg = group_bcast<L, src>(mine[u].tg);
                 // Wave-uniform branch (taken iff the owner lane of this pair rotates it in
                 // some block of the wave); lanes whose block skips this pair apply the identity
                 // (c, s, t*gamma) = (1, 0, 0): fma(-0, y, 1*x) == x bitwise for every value
                 // A (phase 3) and V can hold (their fma chains start from +0 and never make
                 // -0), and A32 / phase-1 A only feed cdot(), which ignores signs of zero.
                 if (!kBranchy || (own_ball[u] & kMemberMask<L, src>) != 0) {
-                    nrm[i] = nrm[i] - tg;
-                    nrm[j] = nrm[j] + tg;
+                    if constexpr (!kLN) {
+                        const T tg = group_bcast<L, src>(mine[u].tg);
+                        nrm[i] = nrm[i] - tg;
+                        nrm[j] = nrm[j] + tg;
+                    }
                     rotate_cols<R, B, WANT_V>(A, V, i, j, c, sn);
                 }
             });
@@ -1043,9 +1102,10 @@ struct NoStamp {
     TMF_DEVI void operator()(int) const {}
 };
 
+// nl: this block's LDS scratch for the column norms (kLdsNorms<L>; 16 doubles, 8-byte aligned)
 template <int B, int L, typename Stamp = NoStamp>
 TMF_DEVI int svd3(const float (&D)[(B + L - 1) / L][B], double (&A)[(B + L - 1) / L][B], double (&V)[(B + L - 1) / L][B], int q,
-                  Stamp stamp = {})
+                  Stamp stamp = {}, void *nl = nullptr)
 {
     constexpr int R = kRows<B, L>;
     int s32;
@@ -1058,7 +1118,7 @@ TMF_DEVI int svd3(const float (&D)[(B + L - 1) / L][B], double (&A)[(B + L - 1) 
                 A32[r][c] = D[r][c];
                 V32[r][c] = (q * R + r == c) ? 1.0f : 0.0f;
             }
-        s32 = jacobi<float, B, L, true>(A32, V32, q);
+        s32 = jacobi<float, B, L, true>(A32, V32, q, static_cast<float *>(nl));
 #pragma unroll
         for (int r = 0; r < R; ++r)
 #pragma unroll
@@ -1069,7 +1129,8 @@ TMF_DEVI int svd3(const float (&D)[(B + L - 1) / L][B], double (&A)[(B + L - 1) 
     bjorck<B, L>(V);
     mul_dv<B, L>(D, V, A);
     stamp(2);
-    const int s64 = jacobi<double, B, L, true>(A, V, q);
+    lds_order();
+    const int s64 = jacobi<double, B, L, true>(A, V, q, static_cast<double *>(nl));
     stamp(3);
     return s64 | (s32 << 8);
 }
