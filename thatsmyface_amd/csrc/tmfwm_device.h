@@ -877,6 +877,22 @@ constexpr bool kLdsNorms = TMF_LDS_NORMS && L >= 2 && L >= TMF_LN_MIN_L;
 #define TMF_LN_TYPES(T) (std::is_same_v<T, double>)
 #endif
 
+// Rotation parameters through LDS (8-lane blocks): the owner of each pair writes its
+// (c, s) next to the norms and every lane of the block reads the pairs it applies
+// (ds_write2 + one ds_read2 per pair), instead of two ds_swizzle per 32-bit half of each
+// broadcast value.  Pure data movement: the same bits.
+#ifndef TMF_LDS_BCAST
+#define TMF_LDS_BCAST 1
+#endif
+#ifndef TMF_LB_TYPES
+#define TMF_LB_TYPES(T) true
+#endif
+#ifndef TMF_LB_MIN_L  // smallest block group that broadcasts through LDS (timing experiments)
+#define TMF_LB_MIN_L 8
+#endif
+template <int L>
+constexpr bool kLdsBcast = TMF_LDS_BCAST && L >= 2 && L >= TMF_LB_MIN_L;
+
 // pair p's lower / higher column for every p < b/2 of round s, one 4-bit field per lane
 // p; a lane without a pair (p >= b/2: b = 14) gets slot 15, a dummy past the b norms
 template <int B, int S, bool HI>
@@ -899,7 +915,12 @@ TMF_DEVI int jacobi(T (&A)[(B + L - 1) / L][B], T (&V)[(B + L - 1) / L][B], int 
     constexpr int R = kRows<B, L>, NP = B / 2, PP = (NP + L - 1) / L;
     constexpr bool kBranchy = P::kBranchy;
     constexpr bool kLN = kLdsNorms<L> && TMF_LN_TYPES(T);
+    constexpr bool kLB = kLdsBcast<L> && TMF_LB_TYPES(T);
     static_assert(!kLN || NP <= 8, "LDS norms: 4-bit pair table");
+    static_assert(!kLB || L * PP <= 8, "LDS broadcast: 8 parameter slots");
+    // kLB: (c, s) of pair slot p at prm[2p], prm[2p+1] (after the 16 norms when those are
+    // in LDS too), t*gamma at prm[16 + p] when the norms are replicated on the lanes
+    T *prm = nl + (kLN ? 16 : 0);
     T F = T(0);
     static_for<B>([&](auto K) { F += cdot<R, B, L>(A, K, K); });
     const T c2 = P::kC2 * F;
@@ -983,10 +1004,25 @@ TMF_DEVI int jacobi(T (&A)[(B + L - 1) / L][B], T (&V)[(B + L - 1) / L][B], int 
                     nl[own_j] = b + mine[U].tg;
                 }
             });
+            if constexpr (kLB) {
+                lds_order();  // after the previous round's reads
+                static_for<PP>([&](auto U) {
+                    prm[2 * (q * PP + U)] = mine[U].c;
+                    prm[2 * (q * PP + U) + 1] = mine[U].s;
+                    if constexpr (!kLN) prm[16 + q * PP + U] = mine[U].tg;
+                });
+                lds_order();
+            }
             static_for<NP>([&](auto Pi) {
                 constexpr int p = Pi, i = Sched<B>::lo(s, p), j = Sched<B>::hi(s, p), u = p % PP, src = p / PP;
-                const T c = group_bcast<L, src>(mine[u].c);
-                const T sn = group_bcast<L, src>(mine[u].s);
+                T c, sn;
+                if constexpr (kLB) {
+                    c = prm[2 * p];
+                    sn = prm[2 * p + 1];
+                } else {
+                    c = group_bcast<L, src>(mine[u].c);
+                    sn = group_bcast<L, src>(mine[u].s);
+                }
                 // Wave-uniform branch (taken iff the owner lane of this pair rotates it in
                 // some block of the wave); lanes whose block skips this pair apply the identity
                 // (c, s, t*gamma) = (1, 0, 0): fma(-0, y, 1*x) == x bitwise for every value
@@ -994,7 +1030,9 @@ TMF_DEVI int jacobi(T (&A)[(B + L - 1) / L][B], T (&V)[(B + L - 1) / L][B], int 
                 // -0), and A32 / phase-1 A only feed cdot(), which ignores signs of zero.
                 if (!kBranchy || (own_ball[u] & kMemberMask<L, src>) != 0) {
                     if constexpr (!kLN) {
-                        const T tg = group_bcast<L, src>(mine[u].tg);
+                        T tg;
+                        if constexpr (kLB) tg = prm[16 + p];
+                        else tg = group_bcast<L, src>(mine[u].tg);
                         nrm[i] = nrm[i] - tg;
                         nrm[j] = nrm[j] + tg;
                     }
@@ -1102,7 +1140,8 @@ struct NoStamp {
     TMF_DEVI void operator()(int) const {}
 };
 
-// nl: this block's LDS scratch for the column norms (kLdsNorms<L>; 16 doubles, 8-byte aligned)
+// nl: this block's LDS scratch for the column norms (kLdsNorms<L>) and the broadcast rotation
+// parameters (kLdsBcast<L>): 32 slots of T, 8-byte aligned
 template <int B, int L, typename Stamp = NoStamp>
 TMF_DEVI int svd3(const float (&D)[(B + L - 1) / L][B], double (&A)[(B + L - 1) / L][B], double (&V)[(B + L - 1) / L][B], int q,
                   Stamp stamp = {}, void *nl = nullptr)
