@@ -163,14 +163,22 @@ TMF_DEVI void load_block_rows(const uint8_t *frame_base, int W, const StripPos &
     }
 }
 
+// Per-channel unit values from a 256-entry LDS table (luma_t / chroma_t) instead of
+// converting every byte: same values, same bits, fewer VALU operations per pixel.
+#ifndef TMF_UNIT_LUT
+#define TMF_UNIT_LUT 0
+#endif
+
 template <int B>
-TMF_DEVI void luma_rows(const uint32_t (&words)[Geo<B>::R][Geo<B>::NW], float (&y)[Geo<B>::R][B])
+TMF_DEVI void luma_rows(const uint32_t (&words)[Geo<B>::R][Geo<B>::NW], float (&y)[Geo<B>::R][B], const double *ut)
 {
 #pragma unroll
     for (int r = 0; r < Geo<B>::R; ++r)
 #pragma unroll
-        for (int c = 0; c < B; ++c)
-            y[r][c] = luma(byte_at(words[r], 3 * c), byte_at(words[r], 3 * c + 1), byte_at(words[r], 3 * c + 2));
+        for (int c = 0; c < B; ++c) {
+            const uint32_t R8 = byte_at(words[r], 3 * c), G8 = byte_at(words[r], 3 * c + 1), B8 = byte_at(words[r], 3 * c + 2);
+            y[r][c] = TMF_UNIT_LUT ? luma_t(ut, R8, G8, B8) : luma(R8, G8, B8);
+        }
 }
 
 // ---------------------------------------------------------------------------
@@ -195,7 +203,9 @@ __global__ __launch_bounds__(64, kEmbedWaves<B>) void embed_kernel(EmbedArgs a)
     constexpr int L = Geo<B>::L, R = Geo<B>::R, BPW = Geo<B>::BPW, LD = B + 1, NW = Geo<B>::NW;
     __shared__ __attribute__((aligned(16))) float lds[BPW * B * LD];  // also the column norms during the SVD
     __shared__ uint32_t pix[R * NW][64];  // this lane's source bytes, parked during the SVD
+    __shared__ double ut[TMF_UNIT_LUT ? 256 : 1];  // unit values of the 256 byte values
     const int lane = threadIdx.x & 63, g = lane / L, q = lane % L;
+    if constexpr (TMF_UNIT_LUT) fill_unit_table(ut, lane);  // read after dct2d's first barrier
     float *tile = lds + g * B * LD;
     const StripPos pos = strip_pos<B>(a.strips_per_row, a.nbw);
     const uint8_t *src = a.src + pos.frame * a.frame_stride;
@@ -206,7 +216,8 @@ __global__ __launch_bounds__(64, kEmbedWaves<B>) void embed_kernel(EmbedArgs a)
     {
         uint32_t words[R][NW];
         load_block_rows<B>(src, a.W, pos, q, a.aligned, words);
-        luma_rows<B>(words, x);
+        if constexpr (TMF_UNIT_LUT) __syncthreads();
+        luma_rows<B>(words, x, ut);
 #pragma unroll
         for (int r = 0; r < R; ++r)
 #pragma unroll
@@ -342,7 +353,9 @@ __global__ __launch_bounds__(64, kEmbedWaves<B>) void embed_kernel(EmbedArgs a)
 #pragma unroll
             for (int c = 0; c < B; ++c) {
                 float cbs, crs;
-                chroma(byte_at(words[r], 3 * c), byte_at(words[r], 3 * c + 1), byte_at(words[r], 3 * c + 2), cbs, crs);
+                const uint32_t R0 = byte_at(words[r], 3 * c), G0 = byte_at(words[r], 3 * c + 1), B0 = byte_at(words[r], 3 * c + 2);
+                if constexpr (TMF_UNIT_LUT) chroma_t(ut, R0, G0, B0, cbs, crs);
+                else chroma(R0, G0, B0, cbs, crs);
                 uint32_t R8, G8, B8;
                 colour_inv(x[r][c], cbs, crs, R8, G8, B8);
                 const int k0 = 3 * c;

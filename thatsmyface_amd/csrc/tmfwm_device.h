@@ -48,6 +48,27 @@ TMF_DEVI void chroma(uint32_t R, uint32_t G, uint32_t B, float &cbs, float &crs)
     crs = (float)__builtin_fma(-0.081, b, __builtin_fma(0.5, r, -0.419 * g)) + 0.5f;
 }
 
+// The same two functions on pre-converted channels: ut[v] == (double)unit_from_u8(v), a
+// 256-entry table in LDS (one ds_read_b64 per channel instead of the byte conversion,
+// the correctly rounded divide and the widening).  Same operations, same bits.
+TMF_DEVI float luma_t(const double *ut, uint32_t R, uint32_t G, uint32_t B)
+{
+    const double r = ut[R], g = ut[G], b = ut[B];
+    return (float)__builtin_fma(0.114, b, __builtin_fma(0.299, r, 0.587 * g));
+}
+TMF_DEVI void chroma_t(const double *ut, uint32_t R, uint32_t G, uint32_t B, float &cbs, float &crs)
+{
+    const double r = ut[R], g = ut[G], b = ut[B];
+    cbs = (float)__builtin_fma(0.5, b, __builtin_fma(-0.169, r, -0.331 * g)) + 0.5f;
+    crs = (float)__builtin_fma(-0.081, b, __builtin_fma(0.5, r, -0.419 * g)) + 0.5f;
+}
+// fill a wave's table: 4 entries per lane
+TMF_DEVI void fill_unit_table(double *ut, int lane)
+{
+#pragma unroll
+    for (int k = 0; k < 4; ++k) ut[lane + 64 * k] = (double)unit_from_u8((uint32_t)(lane + 64 * k));
+}
+
 // np.clip(.,0,1) in f32, * 255 in f32, astype(uint8) = truncation (watermarking.py:70-73).
 // The clip is one v_med3_f32; it differs from np.clip only in the sign of a zero
 // result (and on NaN, which no finite pixel produces), and -0 * 255 truncates to 0 too.
