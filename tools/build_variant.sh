@@ -4,6 +4,7 @@
 # The kernel TUs take the extra flags; with FALLBACK=1 in the environment the dgesdd-route
 # TU (tmfwm_fallback.hip) is recompiled with them too, otherwise the ABI / tile / QR /
 # dgesdd-route objects are the main build's (make -C thatsmyface_amd/csrc first).
+# E8SCHED=<strategy> overrides the machine scheduler of the embed<8> TU (default max-ilp).
 set -euo pipefail
 NAME=$1; shift
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
@@ -12,7 +13,7 @@ make -s -C "$C" >/dev/null
 T=$(mktemp -d)
 F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -fno-slp-vectorize -Wall $*"
 /opt/rocm/bin/hipcc $F -c "$C/tmfwm_kernels.hip" -o "$T/k.o" &
-/opt/rocm/bin/hipcc $F -mllvm -amdgpu-sched-strategy=max-ilp -c "$C/tmfwm_embed8.hip" -o "$T/e8.o" &
+/opt/rocm/bin/hipcc $F -mllvm -amdgpu-sched-strategy=${E8SCHED:-max-ilp} -c "$C/tmfwm_embed8.hip" -o "$T/e8.o" &
 FB="$C/tmfwm_fallback.o $C/tmfwm_fixup4.o $C/tmfwm_fixup6.o $C/tmfwm_fixup8.o $C/tmfwm_fixup10.o $C/tmfwm_fixup12.o $C/tmfwm_fixup14.o $C/tmfwm_fixup16.o"
 if [ "${FALLBACK:-0}" = "1" ]; then
   FB="$T/fb.o"
