@@ -914,6 +914,19 @@ constexpr bool kLdsNorms = TMF_LDS_NORMS && L >= 2 && L >= TMF_LN_MIN_L;
 template <int L>
 constexpr bool kLdsBcast = TMF_LDS_BCAST && L >= 2 && L >= TMF_LB_MIN_L;
 
+// Pair dot products through LDS (8-lane blocks, one pair per lane): only the owner of a
+// pair needs its gamma, so instead of the 3-level DPP butterfly for every pair on every
+// lane, each lane writes its partials and the owner sums its pair's 8 partials in the
+// butterfly's tree order ((p0+p1)+(p2+p3))+((p4+p5)+(p6+p7)) -- the same bits.
+#ifndef TMF_LDS_SUMS
+#define TMF_LDS_SUMS 1
+#endif
+#ifndef TMF_LS_TYPES  // which phases sum through LDS (timing experiments)
+#define TMF_LS_TYPES(T) true
+#endif
+template <int L>
+constexpr bool kLdsSums = TMF_LDS_SUMS && L == 8;
+
 // pair p's lower / higher column for every p < b/2 of round s, one 4-bit field per lane
 // p; a lane without a pair (p >= b/2: b = 14) gets slot 15, a dummy past the b norms
 template <int B, int S, bool HI>
@@ -942,6 +955,8 @@ TMF_DEVI int jacobi(T (&A)[(B + L - 1) / L][B], T (&V)[(B + L - 1) / L][B], int 
     // kLB: (c, s) of pair slot p at prm[2p], prm[2p+1] (after the 16 norms when those are
     // in LDS too), t*gamma at prm[16 + p] when the norms are replicated on the lanes
     T *prm = nl + (kLN ? 16 : 0);
+    constexpr bool kLS = kLdsSums<L> && TMF_LS_TYPES(T) && PP == 1;
+    T *part = nl + 32;  // kLS: partial of pair p from lane k at part[p * 8 + k]
     T F = T(0);
     static_for<B>([&](auto K) { F += cdot<R, B, L>(A, K, K); });
     const T c2 = P::kC2 * F;
@@ -972,7 +987,16 @@ TMF_DEVI int jacobi(T (&A)[(B + L - 1) / L][B], T (&V)[(B + L - 1) / L][B], int 
                 constexpr int p = Pi, i = Sched<B>::lo(s, p), j = Sched<B>::hi(s, p);
                 ga[p] = cdot_part<R, B>(A, i, j);
             });
-            static_for<NP>([&](auto Pi) { ga[Pi] = group_sum<L>(ga[Pi]); });
+            T gown = T(0);  // kLS: this lane's pair's gamma
+            if constexpr (kLS) {
+                lds_order();  // after the previous round's reads
+                static_for<NP>([&](auto Pi) { part[Pi * 8 + q] = ga[Pi]; });
+                lds_order();
+                const T *pp = part + 8 * q;  // lane 7 at b = 14 reads an unused slot: no pair
+                gown = ((pp[0] + pp[1]) + (pp[2] + pp[3])) + ((pp[4] + pp[5]) + (pp[6] + pp[7]));
+            } else {
+                static_for<NP>([&](auto Pi) { ga[Pi] = group_sum<L>(ga[Pi]); });
+            }
             // this lane's pairs: select (alpha, beta, gamma), evaluate the rotation test
             // (only here -- the owner's flag travels with its parameters), rotation
             Rot<T> mine[PP];
@@ -980,7 +1004,7 @@ TMF_DEVI int jacobi(T (&A)[(B + L - 1) / L][B], T (&V)[(B + L - 1) / L][B], int 
             int own_i = 0, own_j = 0;  // kLN: this lane's pair's columns
             static_for<PP>([&](auto U) {
                 constexpr int p0 = U, i0 = Sched<B>::lo(s, p0), j0 = Sched<B>::hi(s, p0);
-                T a, b, g = ga[p0];
+                T a, b, g = kLS ? gown : ga[p0];
                 if constexpr (kLN) {
                     const int pq = q * PP + p0;  // this lane's U-th pair
                     own_i = (int)__builtin_amdgcn_ubfe(sched_nibbles<B, s, false>(), 4 * pq, 4);
@@ -1002,7 +1026,7 @@ TMF_DEVI int jacobi(T (&A)[(B + L - 1) / L][B], T (&V)[(B + L - 1) / L][B], int 
                             a = blend(m, nrm[i], a);
                             b = blend(m, nrm[j], b);
                         }
-                        g = blend(m, ga[p], g);
+                        if constexpr (!kLS) g = blend(m, ga[p], g);
                     } else {
                         slot &= ~m;
                     }
