@@ -922,7 +922,7 @@ constexpr bool kLdsBcast = TMF_LDS_BCAST && L >= 2 && L >= TMF_LB_MIN_L;
 #define TMF_LDS_SUMS 1
 #endif
 #ifndef TMF_LS_TYPES  // which phases sum through LDS (timing experiments)
-#define TMF_LS_TYPES(T) true
+#define TMF_LS_TYPES(T) (std::is_same_v<T, double>)
 #endif
 template <int L>
 constexpr bool kLdsSums = TMF_LDS_SUMS && L == 8;
