@@ -59,6 +59,11 @@ def parse(argv=None):
     p.add_argument("--structured-crops", type=int, default=16,
                    help="block-aligned 960x544 crops timed with the reference's cost model (oracle/structured.py), "
                         "one per host core; 0 = skip")
+    p.add_argument("--lapack-frames", type=int, default=8,
+                   help="frames of the parity sample also checked against the reference's own SVD arithmetic "
+                        "(the oracle's dgesdd route, ~1 s per 4K frame per 16 cores; 0 = skip)")
+    p.add_argument("--pg-timeout", type=float, default=600.0,
+                   help="seconds a rank may wait in a collective before the run fails (N > 1)")
     p.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                    help="process-group backend for N > 1 (nccl = RCCL over xGMI; gloo only to rehearse "
                         "several ranks on one GPU)")
@@ -86,15 +91,50 @@ def _free_port() -> int:
     return port
 
 
+def visible_gpu_count():
+    """GPUs this process could open, counted WITHOUT initialising HIP (no torch.cuda call:
+    a HIP runtime initialised in this process must not precede the fork+exec of the
+    ranks).  KFD topology nodes with SIMDs whose render node exists in /dev/dri (a
+    container only gets the render nodes of its GPUs), narrowed by the *_VISIBLE_DEVICES
+    masks.  None when the topology is unreadable (then the ranks check for themselves)."""
+    import glob
+
+    if not os.path.isdir("/sys/class/kfd"):
+        return 0  # no amdgpu KFD driver: no GPU at all
+    base = "/sys/class/kfd/kfd/topology/nodes"
+    nodes = glob.glob(os.path.join(base, "*", "properties"))
+    if not nodes:
+        return None
+    n = 0
+    for path in nodes:
+        try:
+            with open(path) as f:
+                props = dict(line.split()[:2] for line in f if len(line.split()) >= 2)
+        except OSError:
+            continue
+        if int(props.get("simd_count", "0")) <= 0:
+            continue
+        minor = props.get("drm_render_minor")
+        if minor is not None and not os.path.exists(f"/dev/dri/renderD{minor}"):
+            continue
+        n += 1
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip() != ""]))
+    return n
+
+
 def spawn_ranks(args, argv, script=None) -> int:
     """Launch args.gpus ranks of this script under torch.distributed.run and return their
-    exit status.  Runs before this process makes any GPU call (device_count does not
-    initialise HIP); the ranks are children, never an exec of this process."""
-    import torch
-
+    exit status.  This process makes no GPU call at all (it does not even import torch):
+    the GPU count comes from sysfs (visible_gpu_count), and the ranks are children, never
+    an exec of this process.  torch.distributed.run ends every rank as soon as one fails,
+    and each rank's process group carries a timeout (--pg-timeout), so a failing or stuck
+    rank ends the run with a non-zero status instead of leaving the others in a collective."""
     if args.backend == "nccl":
-        ndev = torch.cuda.device_count()
-        if ndev < args.gpus:
+        ndev = visible_gpu_count()
+        if ndev is not None and ndev < args.gpus:
             print(f"bench.py: --gpus {args.gpus} needs {args.gpus} visible GPUs, this box has {ndev} "
                   "(use --backend gloo to rehearse several ranks on one GPU)", file=sys.stderr, flush=True)
             return 2
@@ -132,6 +172,24 @@ def oracle_check(host_frames, host_tile, out, tiles, block, alpha, threads):
     bad_e = int(sum(not np.array_equal(emb[i], out[i]) for i in range(len(emb))))
     bad_x = int(sum(not np.array_equal(ext[i], tiles[i]) for i in range(len(ext))))
     return dt, bad_e, bad_x
+
+
+def lapack_check(host_frames, host_tile, out, tiles, block, alpha, threads):
+    """The reference's own SVD arithmetic on k frames: every block through the oracle's
+    dgesdd route (np.linalg.svd restated, pinned bit for bit against numpy).  Extract is
+    run on the GPU's watermarked frames, the input the GPU's extract consumed.
+    Returns (frames, embed mismatches, extract mismatches)."""
+    import numpy as np
+
+    from oracle import oracle as O
+
+    bad_e = bad_x = 0
+    for i in range(len(host_frames)):
+        emb = O.embed_frame(host_frames[i], host_tile, block, alpha, threads, route="lapack")
+        ext = O.extract_frame(out[i], host_frames[i], block, alpha, threads, route="lapack")
+        bad_e += int(not np.array_equal(emb, out[i]))
+        bad_x += int(not np.array_equal(ext, tiles[i]))
+    return len(host_frames), bad_e, bad_x
 
 
 def oracle_threads(world: int) -> int:
@@ -217,10 +275,13 @@ def run(args, kernels=None, device=None):
     dev = device
     on_gpu = dev.type == "cuda"
     if world > 1:
+        import datetime
+
+        timeout = datetime.timedelta(seconds=args.pg_timeout)
         if args.backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group("nccl", device_id=dev, timeout=timeout)
         else:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=timeout)
     K = kernels or gpu_kernels()
     sync = torch.cuda.synchronize if on_gpu else (lambda: None)
 
@@ -286,19 +347,31 @@ def run(args, kernels=None, device=None):
     achieved = embed_bytes / (embed_ms * 1e-3) / 1e9
     achieved_read = F * embed_read / (embed_ms * 1e-3) / 1e9
 
-    # parity of the timed batch against the oracle: rank 0 at N = 1 checks the CPU-baseline
-    # sample (its first k frames); at N > 1 every rank checks the last frame of its shard
+    # parity of the timed batch against the oracle.  N = 1: rank 0 checks the CPU-baseline
+    # sample (the batch's first --cpu-frames frames); N > 1: every rank checks its share of
+    # --cpu-frames, spread evenly over its shard.  The first --lapack-frames of the sample
+    # (N > 1: their share per rank) are also checked against the oracle's dgesdd route,
+    # i.e. np.linalg.svd's own arithmetic (tmfwm_lapack.c), not the device contract's
+    # conditioning flag, which the default (hybrid) route shares with the GPU.
     cpu, parity = None, None
     n_local = stop - start
     want_cpu = rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_frames > 0
     checked = bad_e = bad_x = 0
-    if want_cpu or (world > 1 and n_local > 0):
-        idx = list(range(min(args.cpu_frames, n_local))) if want_cpu else [n_local - 1]
+    lp_checked = lp_bad_e = lp_bad_x = 0
+    if want_cpu or (world > 1 and n_local > 0 and args.cpu_frames > 0):
+        if want_cpu:
+            idx = list(range(min(args.cpu_frames, n_local)))
+        else:
+            k = min(n_local, max(1, -(-args.cpu_frames // world)))
+            idx = sorted({int(round(x)) for x in np.linspace(0, n_local - 1, k)})
         threads = oracle_threads(world)
         host = frames[idx].cpu().numpy()
-        dt, bad_e, bad_x = oracle_check(host, wm.cpu().numpy(), rt.out[idx].cpu().numpy(),
-                                        rt.tiles[idx].cpu().numpy(), b, alpha, threads)
+        host_tile = wm.cpu().numpy()
+        gout, gtiles = rt.out[idx].cpu().numpy(), rt.tiles[idx].cpu().numpy()
+        dt, bad_e, bad_x = oracle_check(host, host_tile, gout, gtiles, b, alpha, threads)
         checked = len(idx)
+        n_lp = min(checked, args.lapack_frames if world == 1 else -(-args.lapack_frames // world))
+        lp_checked, lp_bad_e, lp_bad_x = lapack_check(host[:n_lp], host_tile, gout[:n_lp], gtiles[:n_lp], b, alpha, threads)
         if want_cpu:
             cpu = {
                 "value": round(checked * H * W / dt / 1e6, 3),
@@ -310,12 +383,18 @@ def run(args, kernels=None, device=None):
             }
     if world > 1:  # every rank joins, checked or not
         cdev = dev if args.backend == "nccl" else "cpu"
-        counts = torch.tensor([checked, bad_e, bad_x], dtype=torch.int64, device=cdev)
+        counts = torch.tensor([checked, bad_e, bad_x, lp_checked, lp_bad_e, lp_bad_x], dtype=torch.int64, device=cdev)
         dist.all_reduce(counts)
-        checked, bad_e, bad_x = (int(v) for v in counts.cpu())
+        checked, bad_e, bad_x, lp_checked, lp_bad_e, lp_bad_x = (int(v) for v in counts.cpu())
     if checked:
         parity = {"frames": checked, "embed_mismatch": bad_e, "extract_mismatch": bad_x,
                   "summary": f"{checked - max(bad_e, bad_x)}/{checked} frames bit-exact vs oracle"}
+    lapack_sample = None
+    if lp_checked:
+        ok = lp_checked - max(lp_bad_e, lp_bad_x)
+        lapack_sample = {"frames": lp_checked, "embed_mismatch": lp_bad_e, "extract_mismatch": lp_bad_x,
+                         "route": "oracle dgesdd route for every block (np.linalg.svd's arithmetic, tmfwm_lapack.c)",
+                         "summary": f"{ok}/{lp_checked}"}
 
     # the reference's own cost model: per-pixel np.dot colour loops and
     # per-block scipy / LAPACK calls (oracle/structured.py) on block-aligned crops of the
@@ -421,6 +500,8 @@ def run(args, kernels=None, device=None):
                            "extract_GBs": round(extract_bytes / (extract_ms * 1e-3) / 1e9, 2),
                            "extract_valu_issue": valu.get(f"extract_kernel<{b}>")},
             "parity_sample": parity,
+            "lapack_route_sample": lapack_sample["summary"] if lapack_sample else None,
+            "lapack_route_detail": lapack_sample,
             "cpu_baseline": cpu,
             "cpu_baseline_reference_model": structured,
             "lib_build": build,
@@ -432,6 +513,9 @@ def run(args, kernels=None, device=None):
         dist.destroy_process_group()
     if parity and (parity["embed_mismatch"] or parity["extract_mismatch"]):
         print(f"bench.py: parity FAILED on rank {rank}: {parity}", file=sys.stderr, flush=True)
+        return 3
+    if lapack_sample and (lapack_sample["embed_mismatch"] or lapack_sample["extract_mismatch"]):
+        print(f"bench.py: parity vs the dgesdd route FAILED on rank {rank}: {lapack_sample}", file=sys.stderr, flush=True)
         return 3
     return 0
 

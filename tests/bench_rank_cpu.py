@@ -5,6 +5,10 @@ ranges, tile broadcast, barriers, max-over-ranks timing, parity all-reduce, the 
 line) runs unchanged; only the per-rank kernels are the oracle's, on CPU tensors,
 because this container has no GPU.  Each rank saves its shard's outputs to
 $TMF_BENCH_DUMP so the test can compare the union with a serial oracle run.
+
+TMF_BENCH_FAIL="<rank>:<mode>" injects a failure into one rank's timed embed: "raise"
+(an exception), "parity" (one corrupted output byte) or "hang" (the rank never returns;
+the others must end through the process-group timeout).
 """
 import os
 import sys
@@ -32,9 +36,22 @@ def main():
         state["frame0"] = frame0
         return torch.from_numpy(O.synth_bytes(SEED_COVER, frame0, n, h * w * 3).reshape(n, h, w, 3))
 
+    fail_rank, _, fail_mode = os.environ.get("TMF_BENCH_FAIL", "-1:").partition(":")
+    calls = [0]
+
     def embed(f, t, b, a, o):
         o.copy_(torch.from_numpy(O.embed_batch(f.numpy(), t.numpy(), b, a, 1)))
         state["tile"] = t.numpy().copy()
+        calls[0] += 1
+        if rank == int(fail_rank) and calls[0] > args.warmup:
+            if fail_mode == "raise":
+                raise RuntimeError(f"injected failure on rank {rank}")
+            if fail_mode == "parity":
+                o.view(-1)[0] ^= 1
+            if fail_mode == "hang":
+                import time
+
+                time.sleep(3600)
 
     def extract(w, o, b, a, out):
         out.copy_(torch.from_numpy(O.extract_batch(w.numpy(), o.numpy(), b, a, 1)))
