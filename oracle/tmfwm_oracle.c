@@ -866,6 +866,124 @@ static int jacobi(double *A, double *V, int b, int want_v)
     return sweep;
 }
 
+static void mul_dv(const float *D, const double *V, double *A, int b)
+{
+    for (int r = 0; r < b; ++r)
+        for (int k = 0; k < b; ++k) {
+            double acc = 0.0;
+            for (int j = 0; j < b; ++j) acc = fma((double)D[r * b + j], V[j * b + k], acc);
+            A[r * b + k] = acc;
+        }
+}
+
+/* One sweep of the f64 Jacobi of jacobi() (same schedule, tests and rotation); returns 1
+ * if it rotated a pair. */
+static int jacobi_sweep(double *A, double *V, int b, double c2)
+{
+    int rotated = 0;
+    double nrm[ORC_MAXB];
+    for (int k = 0; k < b; ++k) nrm[k] = cdot(A + k, A + k, b, b);
+    for (int st = 0; st < b - 1; ++st)
+        for (int p = 0; p < b / 2; ++p) {
+            int i, j;
+            jac_pairs(b, st, p, &i, &j);
+            const double alpha = nrm[i], beta = nrm[j];
+            const double gamma = cdot(A + i, A + j, b, b);
+            const double g2 = gamma * gamma;
+            if (g2 <= c2 * (alpha + beta) || g2 <= (JAC_TOL2 * alpha) * beta) continue;
+            rotated = 1;
+            double c, sn, tg;
+            rotation(alpha, beta, gamma, &c, &sn, &tg);
+            nrm[i] = alpha - tg;
+            nrm[j] = beta + tg;
+            for (int r = 0; r < b; ++r) {
+                const double x = A[r * b + i], y = A[r * b + j];
+                A[r * b + i] = fma(-sn, y, c * x);
+                A[r * b + j] = fma(sn, x, c * y);
+            }
+            for (int r = 0; r < b; ++r) {
+                const double x = V[r * b + i], y = V[r * b + j];
+                V[r * b + i] = fma(-sn, y, c * x);
+                V[r * b + j] = fma(sn, x, c * y);
+            }
+        }
+    return rotated;
+}
+
+/* ---- Phase 3 with a Newton finish, b <= 8 -----------------------------
+ * Once a sweep has left only tiny couplings, one first-order Newton step replaces the
+ * sweeps that would follow (typically a rotating sweep of tiny angles plus the sweep that
+ * finds nothing to rotate).  With V orthogonal to rounding level and A = D V, the step
+ * V' = V (I + F), A' = A (I + F) with
+ *     F_ij = f32(G_ij) / f32(G_jj - G_ii),  F_ji = -F_ij  (i < j),  F_kk = 0,  G = A^T A
+ * (contract dots; IEEE f32 divide; a coupling the Jacobi's own tests would not rotate --
+ * relative 2^-50, noise floor 2^-103 F (alpha+beta) -- gives F_ij = 0) makes A'^T A'
+ * diagonal to second order.  It is taken, and ends the block, only when every
+ * |F_ij| <= 2^-27: the neglected terms (second order in F, and (I+F)^T (I+F) - I = -F^2)
+ * are then below f64 rounding (times the gap amplification every f64 method carries).
+ * The correction X F is formed in f32 from f32(X) (fma chain over i != j; its error,
+ * <= ~2^-24 |X| |F|, is below f64 rounding at that size) and added in f64.  Otherwise
+ * the block takes the next sweep.  Per block: sweep; if it rotated nothing, done (the
+ * Jacobi's own test); Newton try; repeat (at most JAC_MAX_SWEEPS sweeps). */
+#define NWT_MAX_B 8
+#define NWT_APPLY 7.450580596923828e-09f /* 2^-27 */
+static int g_newton_finish = 1; /* 0: phase 3 = jacobi() for every b (studies only: tools/exp) */
+void orc_set_newton_finish(int on) { g_newton_finish = on; }
+
+/* X <- X + f64(f32(X) F) row by row (fma chain over i != j in f32) */
+static void apply_f(double *X, const float *F, int b)
+{
+    for (int r = 0; r < b; ++r) {
+        float xr[ORC_MAXB], cr[ORC_MAXB];
+        for (int i = 0; i < b; ++i) xr[i] = (float)X[r * b + i];
+        for (int j = 0; j < b; ++j) {
+            float acc = 0.0f;
+            for (int i = 0; i < b; ++i)
+                if (i != j) acc = fmaf(xr[i], F[i * b + j], acc);
+            cr[j] = acc;
+        }
+        for (int j = 0; j < b; ++j) X[r * b + j] = X[r * b + j] + (double)cr[j];
+    }
+}
+
+/* Returns 1 if the step was taken (the block is done). */
+static int newton_try(double *A, double *V, int b, double c2)
+{
+    double G[ORC_MAXB];
+    float F[ORC_MAXB * ORC_MAXB];
+    int ok = 1;
+    for (int k = 0; k < b; ++k) G[k] = cdot(A + k, A + k, b, b);
+    for (int i = 0; i < b; ++i) {
+        F[i * b + i] = 0.0f;
+        for (int j = i + 1; j < b; ++j) {
+            const double g = cdot(A + i, A + j, b, b), g2 = g * g;
+            float f = 0.0f;
+            if (!(g2 <= c2 * (G[i] + G[j]) || g2 <= (JAC_TOL2 * G[i]) * G[j])) f = (float)g / (float)(G[j] - G[i]);
+            F[i * b + j] = f;
+            F[j * b + i] = -f;
+            ok &= fabsf(f) <= NWT_APPLY; /* NaN / inf fail */
+        }
+    }
+    if (!ok) return 0;
+    apply_f(V, F, b);
+    apply_f(A, F, b);
+    return 1;
+}
+
+/* returns sweeps | (Newton steps << 16) */
+static int jacobi_newton(double *A, double *V, int b)
+{
+    double F = 0.0;
+    for (int k = 0; k < b; ++k) F += cdot(A + k, A + k, b, b);
+    const double c2 = JAC_C2 * F;
+    int sweeps;
+    for (sweeps = 1; sweeps <= JAC_MAX_SWEEPS; ++sweeps) {
+        if (!jacobi_sweep(A, V, b, c2)) break;
+        if (newton_try(A, V, b, c2)) return sweeps | (1 << 16);
+    }
+    return sweeps > JAC_MAX_SWEEPS ? JAC_MAX_SWEEPS : sweeps;
+}
+
 /* Full SVD of one block in f64, before rounding: D (b x b f32 row-major) -> U (b x b,
  * u[r][k]), sig (b), V (b x b, v[r][k]), sorted by descending sig.  Zero block: U = V = I.
  * Returns the sweeps done: f64 sweeps | (f32 sweeps << 8). */
@@ -882,19 +1000,17 @@ int orc_svd_block_f64(const float *D, int b, double *U, double *sig, double *V)
         return 0;
     }
     /* phase 1: f32 Jacobi on D; phase 2: V0 = Bjorck^2(f64(V32)); phase 3: f64
-     * Jacobi on A0 = D V0 (fma chain over j), accumulating onto V0 */
+     * Jacobi on A0 = D V0 (fma chain over j), accumulating onto V0 (b <= 8: with the
+     * Newton finish) */
     float A32[ORC_MAXB * ORC_MAXB], V32[ORC_MAXB * ORC_MAXB];
     for (int k = 0; k < b * b; ++k) { A32[k] = D[k]; V32[k] = (k / b == k % b) ? 1.0f : 0.0f; }
     const int s32 = jacobi_f32(A32, V32, b);
     for (int k = 0; k < b * b; ++k) V[k] = V32[k];
+    int sweeps;
     for (int it = 0; it < JAC_BJORCK_STEPS; ++it) bjorck(V, b);
-    for (int r = 0; r < b; ++r)
-        for (int k = 0; k < b; ++k) {
-            double acc = 0.0;
-            for (int j = 0; j < b; ++j) acc = fma((double)D[r * b + j], V[j * b + k], acc);
-            A[r * b + k] = acc;
-        }
-    const int sweeps = jacobi(A, V, b, 1) | (s32 << 8);
+    mul_dv(D, V, A, b);
+    if (b <= NWT_MAX_B && g_newton_finish) sweeps = jacobi_newton(A, V, b) | (s32 << 8);
+    else sweeps = jacobi(A, V, b, 1) | (s32 << 8);
     for (int k = 0; k < b; ++k) {
         sig[k] = sqrt(cdot(A + k, A + k, b, b));
         if (sig[k] == 0.0) {

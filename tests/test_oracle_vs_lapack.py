@@ -58,4 +58,4 @@ def test_svd_factors_close_to_lapack():
     sg = np.sign(np.sum(U * u, axis=1, keepdims=True))
     assert np.abs(U - u * sg).max() <= 2.0**-22
     assert np.abs(Vt - vt * np.swapaxes(sg, 1, 2)).max() <= 2.0**-22
-    assert ((sw >> 8) <= 4).all() and ((sw & 0xFF) <= 32).all()
+    assert (((sw >> 8) & 0xFF) <= 4).all() and ((sw & 0xFF) <= 32).all() and (((sw >> 16) & 0xFF) <= 32).all()

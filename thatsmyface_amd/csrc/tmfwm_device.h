@@ -941,8 +941,13 @@ constexpr uint32_t sched_nibbles()
 // (the lanes of a wave see each other's LDS writes in program order)
 TMF_DEVI void lds_order() { asm volatile("" ::: "memory"); }
 
+// One sweep (oracle jacobi_sweep() / the loop body of jacobi()): nrm are recomputed, the
+// b-1 rounds of b/2 disjoint pairs rotate every pair that passes the tests.  `enable`
+// (same on the L lanes of a block) adds "skip" to every test of this block's pairs: a
+// disabled block takes the identity on every pair, bitwise.  Returns 1 on a lane that
+// rotated one of its own pairs (group_or over the block = the block rotated).
 template <typename T, int B, int L, bool WANT_V>
-TMF_DEVI int jacobi(T (&A)[(B + L - 1) / L][B], T (&V)[(B + L - 1) / L][B], int q, T *nl = nullptr)
+TMF_DEVI int jacobi_sweep(T (&A)[(B + L - 1) / L][B], T (&V)[(B + L - 1) / L][B], int q, T *nl, T c2, T c2a, bool enable)
 {
     using P = JacP<T>;
     // NP pairs per round; lane q evaluates pairs [q*PP, q*PP + PP) that exist
@@ -957,8 +962,139 @@ TMF_DEVI int jacobi(T (&A)[(B + L - 1) / L][B], T (&V)[(B + L - 1) / L][B], int 
     T *prm = nl + (kLN ? 16 : 0);
     constexpr bool kLS = kLdsSums<L> && TMF_LS_TYPES(T) && PP == 1;
     T *part = nl + 32;  // kLS: partial of pair p from lane k at part[p * 8 + k]
+    T nrm[B];
+    // batches of dot products: all lane-local chains first, then all cross-lane sums,
+    // so that the chains interleave and no DPP read waits on the write just before it
+    static_for<B>([&](auto K) { nrm[K] = cdot_part<R, B>(A, K, K); });
+    static_for<B>([&](auto K) { nrm[K] = group_sum<L>(nrm[K]); });
+    if constexpr (kLN) {
+        lds_order();
+        if (q == 0) static_for<B>([&](auto K) { nl[K] = nrm[K]; });
+        lds_order();
+    }
+    int rotated = 0;  // this lane rotated one of its own pairs this sweep
+    static_for<B - 1>([&](auto S) {
+        constexpr int s = S;
+        T ga[NP];
+        static_for<NP>([&](auto Pi) {
+            constexpr int p = Pi, i = Sched<B>::lo(s, p), j = Sched<B>::hi(s, p);
+            ga[p] = cdot_part<R, B>(A, i, j);
+        });
+        T gown = T(0);  // kLS: this lane's pair's gamma
+        if constexpr (kLS) {
+            lds_order();  // after the previous round's reads
+            static_for<NP>([&](auto Pi) { part[Pi * 8 + q] = ga[Pi]; });
+            lds_order();
+            const T *pp = part + 8 * q;  // lane 7 at b = 14 reads an unused slot: no pair
+            gown = ((pp[0] + pp[1]) + (pp[2] + pp[3])) + ((pp[4] + pp[5]) + (pp[6] + pp[7]));
+        } else {
+            static_for<NP>([&](auto Pi) { ga[Pi] = group_sum<L>(ga[Pi]); });
+        }
+        // this lane's pairs: select (alpha, beta, gamma), evaluate the rotation test
+        // (only here -- the owner's flag travels with its parameters), rotation
+        Rot<T> mine[PP];
+        unsigned long long own_ball[PP];  // wave mask of the lanes whose U-th pair rotates
+        int own_i = 0, own_j = 0;  // kLN: this lane's pair's columns
+        static_for<PP>([&](auto U) {
+            constexpr int p0 = U, i0 = Sched<B>::lo(s, p0), j0 = Sched<B>::hi(s, p0);
+            T a, b, g = kLS ? gown : ga[p0];
+            if constexpr (kLN) {
+                const int pq = q * PP + p0;  // this lane's U-th pair
+                own_i = (int)__builtin_amdgcn_ubfe(sched_nibbles<B, s, false>(), 4 * pq, 4);
+                own_j = (int)__builtin_amdgcn_ubfe(sched_nibbles<B, s, true>(), 4 * pq, 4);
+                a = nl[own_i];
+                b = nl[own_j];
+            } else {
+                a = nrm[i0];
+                b = nrm[j0];
+            }
+            int slot = -1;  // lane has a U-th pair this round
+            static_for<L - 1>([&](auto Q1) {
+                constexpr int QQ = Q1 + 1, p = QQ * PP + U;
+                int m = -(int)(q == QQ);
+                asm volatile("" : "+v"(m));
+                if constexpr (p < NP) {
+                    constexpr int i = Sched<B>::lo(s, p), j = Sched<B>::hi(s, p);
+                    if constexpr (!kLN) {
+                        a = blend(m, nrm[i], a);
+                        b = blend(m, nrm[j], b);
+                    }
+                    if constexpr (!kLS) g = blend(m, ga[p], g);
+                } else {
+                    slot &= ~m;
+                }
+            });
+            const T g2 = g * g;
+            bool skip = g2 <= c2 * (a + b) || g2 <= (P::kTol2 * a) * b || !enable;
+            if constexpr (std::is_same_v<T, float>) skip = skip || g2 <= c2a;
+            const bool o = slot != 0 && !skip;
+            own_ball[U] = __ballot(o);
+            rotated |= (int)o;
+            mine[U] = Rot<T>{T(1), T(0), T(0)};
+            if (!kBranchy || __any(o)) {  // wave-uniform: every lane computes, non-rotating lanes keep identity
+                const Rot<T> r = rotation(a, b, g);
+                mine[U].c = o ? r.c : T(1);
+                mine[U].s = o ? r.s : T(0);
+                mine[U].tg = o ? r.tg : T(0);
+            }
+            if constexpr (kLN) {  // every lane writes its pair's norms back: old value -+ t*gamma
+                nl[own_i] = a - mine[U].tg;  // (t*gamma = 0 when it does not rotate: the same bits)
+                nl[own_j] = b + mine[U].tg;
+            }
+        });
+        if constexpr (kLB) {
+            lds_order();  // after the previous round's reads
+            static_for<PP>([&](auto U) {
+                prm[2 * (q * PP + U)] = mine[U].c;
+                prm[2 * (q * PP + U) + 1] = mine[U].s;
+                if constexpr (!kLN) prm[16 + q * PP + U] = mine[U].tg;
+            });
+            lds_order();
+        }
+        static_for<NP>([&](auto Pi) {
+            constexpr int p = Pi, i = Sched<B>::lo(s, p), j = Sched<B>::hi(s, p), u = p % PP, src = p / PP;
+            T c, sn;
+            if constexpr (kLB) {
+                c = prm[2 * p];
+                sn = prm[2 * p + 1];
+            } else {
+                c = group_bcast<L, src>(mine[u].c);
+                sn = group_bcast<L, src>(mine[u].s);
+            }
+            // Wave-uniform branch (taken iff the owner lane of this pair rotates it in
+            // some block of the wave); lanes whose block skips this pair apply the identity
+            // (c, s, t*gamma) = (1, 0, 0): fma(-0, y, 1*x) == x bitwise for every value
+            // A (phase 3) and V can hold (their fma chains start from +0 and never make
+            // -0), and A32 / phase-1 A only feed cdot(), which ignores signs of zero.
+            if (!kBranchy || (own_ball[u] & kMemberMask<L, src>) != 0) {
+                if constexpr (!kLN) {
+                    T tg;
+                    if constexpr (kLB) tg = prm[16 + p];
+                    else tg = group_bcast<L, src>(mine[u].tg);
+                    nrm[i] = nrm[i] - tg;
+                    nrm[j] = nrm[j] + tg;
+                }
+                rotate_cols<R, B, WANT_V>(A, V, i, j, c, sn);
+            }
+        });
+    });
+    return rotated;
+}
+
+// F = |A|_F^2 (contract dots) and the Jacobi's noise-floor constants
+template <typename T, int B, int L>
+TMF_DEVI T frob2(const T (&A)[(B + L - 1) / L][B])
+{
     T F = T(0);
-    static_for<B>([&](auto K) { F += cdot<R, B, L>(A, K, K); });
+    static_for<B>([&](auto K) { F += cdot<kRows<B, L>, B, L>(A, K, K); });
+    return F;
+}
+
+template <typename T, int B, int L, bool WANT_V>
+TMF_DEVI int jacobi(T (&A)[(B + L - 1) / L][B], T (&V)[(B + L - 1) / L][B], int q, T *nl = nullptr)
+{
+    using P = JacP<T>;
+    const T F = frob2<T, B, L>(A);
     const T c2 = P::kC2 * F;
     T c2a = T(0);
     bool live = true;
@@ -969,127 +1105,97 @@ TMF_DEVI int jacobi(T (&A)[(B + L - 1) / L][B], T (&V)[(B + L - 1) / L][B], int 
     int count = 0;
     bool active = live;
     for (int sweep = 0; sweep < P::kMaxSweeps; ++sweep) {
-        T nrm[B];
-        // batches of dot products: all lane-local chains first, then all cross-lane sums,
-        // so that the chains interleave and no DPP read waits on the write just before it
-        static_for<B>([&](auto K) { nrm[K] = cdot_part<R, B>(A, K, K); });
-        static_for<B>([&](auto K) { nrm[K] = group_sum<L>(nrm[K]); });
-        if constexpr (kLN) {
-            lds_order();
-            if (q == 0) static_for<B>([&](auto K) { nl[K] = nrm[K]; });
-            lds_order();
-        }
-        int rotated = 0;  // this lane rotated one of its own pairs this sweep
-        static_for<B - 1>([&](auto S) {
-            constexpr int s = S;
-            T ga[NP];
-            static_for<NP>([&](auto Pi) {
-                constexpr int p = Pi, i = Sched<B>::lo(s, p), j = Sched<B>::hi(s, p);
-                ga[p] = cdot_part<R, B>(A, i, j);
-            });
-            T gown = T(0);  // kLS: this lane's pair's gamma
-            if constexpr (kLS) {
-                lds_order();  // after the previous round's reads
-                static_for<NP>([&](auto Pi) { part[Pi * 8 + q] = ga[Pi]; });
-                lds_order();
-                const T *pp = part + 8 * q;  // lane 7 at b = 14 reads an unused slot: no pair
-                gown = ((pp[0] + pp[1]) + (pp[2] + pp[3])) + ((pp[4] + pp[5]) + (pp[6] + pp[7]));
-            } else {
-                static_for<NP>([&](auto Pi) { ga[Pi] = group_sum<L>(ga[Pi]); });
-            }
-            // this lane's pairs: select (alpha, beta, gamma), evaluate the rotation test
-            // (only here -- the owner's flag travels with its parameters), rotation
-            Rot<T> mine[PP];
-            unsigned long long own_ball[PP];  // wave mask of the lanes whose U-th pair rotates
-            int own_i = 0, own_j = 0;  // kLN: this lane's pair's columns
-            static_for<PP>([&](auto U) {
-                constexpr int p0 = U, i0 = Sched<B>::lo(s, p0), j0 = Sched<B>::hi(s, p0);
-                T a, b, g = kLS ? gown : ga[p0];
-                if constexpr (kLN) {
-                    const int pq = q * PP + p0;  // this lane's U-th pair
-                    own_i = (int)__builtin_amdgcn_ubfe(sched_nibbles<B, s, false>(), 4 * pq, 4);
-                    own_j = (int)__builtin_amdgcn_ubfe(sched_nibbles<B, s, true>(), 4 * pq, 4);
-                    a = nl[own_i];
-                    b = nl[own_j];
-                } else {
-                    a = nrm[i0];
-                    b = nrm[j0];
-                }
-                int slot = -1;  // lane has a U-th pair this round
-                static_for<L - 1>([&](auto Q1) {
-                    constexpr int QQ = Q1 + 1, p = QQ * PP + U;
-                    int m = -(int)(q == QQ);
-                    asm volatile("" : "+v"(m));
-                    if constexpr (p < NP) {
-                        constexpr int i = Sched<B>::lo(s, p), j = Sched<B>::hi(s, p);
-                        if constexpr (!kLN) {
-                            a = blend(m, nrm[i], a);
-                            b = blend(m, nrm[j], b);
-                        }
-                        if constexpr (!kLS) g = blend(m, ga[p], g);
-                    } else {
-                        slot &= ~m;
-                    }
-                });
-                const T g2 = g * g;
-                bool skip = g2 <= c2 * (a + b) || g2 <= (P::kTol2 * a) * b;
-                if constexpr (std::is_same_v<T, float>) skip = skip || g2 <= c2a || !live;
-                const bool o = slot != 0 && !skip;
-                own_ball[U] = __ballot(o);
-                rotated |= (int)o;
-                mine[U] = Rot<T>{T(1), T(0), T(0)};
-                if (!kBranchy || __any(o)) {  // wave-uniform: every lane computes, non-rotating lanes keep identity
-                    const Rot<T> r = rotation(a, b, g);
-                    mine[U].c = o ? r.c : T(1);
-                    mine[U].s = o ? r.s : T(0);
-                    mine[U].tg = o ? r.tg : T(0);
-                }
-                if constexpr (kLN) {  // every lane writes its pair's norms back: old value -+ t*gamma
-                    nl[own_i] = a - mine[U].tg;  // (t*gamma = 0 when it does not rotate: the same bits)
-                    nl[own_j] = b + mine[U].tg;
-                }
-            });
-            if constexpr (kLB) {
-                lds_order();  // after the previous round's reads
-                static_for<PP>([&](auto U) {
-                    prm[2 * (q * PP + U)] = mine[U].c;
-                    prm[2 * (q * PP + U) + 1] = mine[U].s;
-                    if constexpr (!kLN) prm[16 + q * PP + U] = mine[U].tg;
-                });
-                lds_order();
-            }
-            static_for<NP>([&](auto Pi) {
-                constexpr int p = Pi, i = Sched<B>::lo(s, p), j = Sched<B>::hi(s, p), u = p % PP, src = p / PP;
-                T c, sn;
-                if constexpr (kLB) {
-                    c = prm[2 * p];
-                    sn = prm[2 * p + 1];
-                } else {
-                    c = group_bcast<L, src>(mine[u].c);
-                    sn = group_bcast<L, src>(mine[u].s);
-                }
-                // Wave-uniform branch (taken iff the owner lane of this pair rotates it in
-                // some block of the wave); lanes whose block skips this pair apply the identity
-                // (c, s, t*gamma) = (1, 0, 0): fma(-0, y, 1*x) == x bitwise for every value
-                // A (phase 3) and V can hold (their fma chains start from +0 and never make
-                // -0), and A32 / phase-1 A only feed cdot(), which ignores signs of zero.
-                if (!kBranchy || (own_ball[u] & kMemberMask<L, src>) != 0) {
-                    if constexpr (!kLN) {
-                        T tg;
-                        if constexpr (kLB) tg = prm[16 + p];
-                        else tg = group_bcast<L, src>(mine[u].tg);
-                        nrm[i] = nrm[i] - tg;
-                        nrm[j] = nrm[j] + tg;
-                    }
-                    rotate_cols<R, B, WANT_V>(A, V, i, j, c, sn);
-                }
-            });
-        });
+        const int rotated = jacobi_sweep<T, B, L, WANT_V>(A, V, q, nl, c2, c2a, live);
         count += active ? 1 : 0;
         active = active && group_or<L>(rotated) != 0;  // block rotated a pair this sweep
         if (!__any(rotated)) break;
     }
     return count;
+}
+
+// ---- Phase 3 with a Newton finish, b <= 8 (oracle jacobi_newton() / newton_try(),
+// DESIGN.md 3.4): after each rotating sweep, F_ij = f32(G_ij) / f32(G_jj - G_ii) over the
+// pairs the Jacobi's tests would rotate (G = A^T A); if every |F_ij| <= 2^-27 the block
+// takes V <- V (I + F), A <- A (I + F) -- the correction formed in f32 -- and is done,
+// otherwise it takes the next sweep.
+constexpr int kNewtonMaxB = 8;
+constexpr float kNwtApply = 7.450580596923828e-09f;  // 2^-27
+
+// upper-triangle index of pair (i, j), i < j
+template <int B>
+constexpr int tri(int i, int j) { return i * B - i * (i + 1) / 2 + (j - i - 1); }
+
+// X <- X + f64(f32(X) F) on this lane's rows, F antisymmetric (upper triangle in F[],
+// diagonal 0): fma chain over i != j, as the oracle's apply_f().  `take` false: unchanged.
+template <int B, int L>
+TMF_DEVI void apply_f(double (&X)[(B + L - 1) / L][B], const float (&F)[B * (B - 1) / 2], bool take)
+{
+    constexpr int R = kRows<B, L>;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        float xr[B];
+#pragma unroll
+        for (int i = 0; i < B; ++i) xr[i] = (float)X[r][i];
+#pragma unroll
+        for (int j = 0; j < B; ++j) {
+            float acc = 0.0f;
+#pragma unroll
+            for (int i = 0; i < B; ++i) {
+                if (i < j) acc = __builtin_fmaf(xr[i], F[tri<B>(i, j)], acc);
+                else if (i > j) acc = __builtin_fmaf(-xr[i], F[tri<B>(j, i)], acc);
+            }
+            X[r][j] = take ? X[r][j] + (double)acc : X[r][j];
+        }
+    }
+}
+
+// Returns true if the step was taken (same on the L lanes of a block; never when !enable).
+template <int B, int L>
+TMF_DEVI bool newton_try(double (&A)[(B + L - 1) / L][B], double (&V)[(B + L - 1) / L][B], double c2, bool enable)
+{
+    constexpr int R = kRows<B, L>, NP = B * (B - 1) / 2;
+    double G[B];
+    static_for<B>([&](auto K) { G[K] = cdot_part<R, B>(A, K, K); });
+    static_for<B>([&](auto K) { G[K] = group_sum<L>(G[K]); });
+    float F[NP];
+    bool ok = enable;
+    static_for<B>([&](auto I) {
+        constexpr int i = I;
+        static_for<B - 1 - i>([&](auto J0) {
+            constexpr int j = i + 1 + J0, p = tri<B>(i, j);
+            const double g = cdot<R, B, L>(A, i, j), g2 = g * g;
+            const bool rot = !(g2 <= c2 * (G[i] + G[j]) || g2 <= (JacP<double>::kTol2 * G[i]) * G[j]);
+            F[p] = rot ? (float)g / (float)(G[j] - G[i]) : 0.0f;
+            ok = ok && __builtin_fabsf(F[p]) <= kNwtApply;  // NaN / inf fail
+        });
+    });
+    if (__any(ok)) {
+        apply_f<B, L>(V, F, ok);
+        apply_f<B, L>(A, F, ok);
+    }
+    return ok;
+}
+
+// oracle jacobi_newton(): returns sweeps | (Newton steps << 16)
+template <int B, int L>
+TMF_DEVI int jacobi_newton(double (&A)[(B + L - 1) / L][B], double (&V)[(B + L - 1) / L][B], int q)
+{
+    static_assert(B <= kNewtonMaxB, "Newton finish: b <= 8");
+    const double c2 = JacP<double>::kC2 * frob2<double, B, L>(A);
+    bool active = true;
+    int sweeps = 0, newton = 0;
+    for (int it = 0; it < JacP<double>::kMaxSweeps; ++it) {
+        const int rotated = jacobi_sweep<double, B, L, true>(A, V, q, nullptr, c2, 0.0, active);
+        sweeps += active ? 1 : 0;
+        active = active && group_or<L>(rotated) != 0;
+        if (!__any(active)) break;
+        if (newton_try<B, L>(A, V, c2, active)) {
+            newton = 1;
+            active = false;
+        }
+        if (!__any(active)) break;
+    }
+    return sweeps | (newton << 16);
 }
 
 // Phase 2 (oracle bjorck()): V <- V N, N = 1.5 I - 0.5 V^T V.  N is symmetric and
@@ -1214,7 +1320,9 @@ TMF_DEVI int svd3(const float (&D)[(B + L - 1) / L][B], double (&A)[(B + L - 1) 
     mul_dv<B, L>(D, V, A);
     stamp(2);
     lds_order();
-    const int s64 = jacobi<double, B, L, true>(A, V, q, static_cast<double *>(nl));
+    int s64;
+    if constexpr (B <= kNewtonMaxB) s64 = jacobi_newton<B, L>(A, V, q);
+    else s64 = jacobi<double, B, L, true>(A, V, q, static_cast<double *>(nl));
     stamp(3);
     return s64 | (s32 << 8);
 }
