@@ -1025,8 +1025,9 @@ TMF_DEVI int jacobi_sweep(T (&A)[(B + L - 1) / L][B], T (&V)[(B + L - 1) / L][B]
                 }
             });
             const T g2 = g * g;
-            bool skip = g2 <= c2 * (a + b) || g2 <= (P::kTol2 * a) * b || !enable;
-            if constexpr (std::is_same_v<T, float>) skip = skip || g2 <= c2a;
+            // every test evaluated (bitwise |): a short-circuit || becomes exec-mask branches
+            bool skip = (g2 <= c2 * (a + b)) | (g2 <= (P::kTol2 * a) * b) | !enable;
+            if constexpr (std::is_same_v<T, float>) skip = skip | (g2 <= c2a);
             const bool o = slot != 0 && !skip;
             own_ball[U] = __ballot(o);
             rotated |= (int)o;

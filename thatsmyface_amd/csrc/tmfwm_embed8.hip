@@ -8,3 +8,16 @@
 namespace tmf {
 template __global__ void embed_kernel<8>(EmbedArgs);
 }  // namespace tmf
+
+#ifdef TMF_STAMPS
+// phase stamps of this TU's embed_kernel<8> (its own copy of g_stamps; tools/phase_stamps.py)
+extern "C" int tmfwm_debug_stamps_e8(unsigned long long *out, int reset)
+{
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(tmf::g_stamps), sizeof(unsigned long long) * 16) != hipSuccess) return -5;
+    if (reset) {
+        unsigned long long z[16] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(tmf::g_stamps), z, sizeof z) != hipSuccess) return -5;
+    }
+    return 0;
+}
+#endif

@@ -14,7 +14,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-os.environ["TMFWM_LIB"] = os.path.join(ROOT, "thatsmyface_amd", "libtmfwm_stamps.so")
+os.environ["TMFWM_LIB"] = os.environ.get("TMF_STAMPS_LIB") or os.path.join(ROOT, "thatsmyface_amd", "libtmfwm_stamps.so")
 
 import torch  # noqa: E402
 
@@ -35,17 +35,19 @@ def main():
     frames = batch.synth_frames(a.frames, a.height, a.width, device=dev)
     tile = batch.synth_tile(a.height // b, a.width // b, device=dev)
     L = _lib.load()
-    L.tmfwm_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    # embed_kernel<8> lives in its own TU (tmfwm_embed8.hip) with its own copy of the stamps
+    rd = L.tmfwm_debug_stamps_e8 if b == 8 and hasattr(L, "tmfwm_debug_stamps_e8") else L.tmfwm_debug_stamps
+    rd.argtypes = [ctypes.c_void_p, ctypes.c_int]
     buf = (ctypes.c_ulonglong * 16)()
     out = batch.embed_batch(frames, tile, b, 0.1)
     torch.cuda.synchronize()
-    L.tmfwm_debug_stamps(buf, 1)
+    rd(buf, 1)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ev0.record()
     batch.embed_batch(frames, tile, b, 0.1, out=out)
     ev1.record()
     torch.cuda.synchronize()
-    L.tmfwm_debug_stamps(buf, 1)
+    rd(buf, 1)
     bpw = {4: 64, 8: 32, 16: 8}[b]
     nbw, nbh = a.width // b, a.height // b
     gx = nbh * ((nbw + bpw - 1) // bpw)
