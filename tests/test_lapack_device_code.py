@@ -32,7 +32,7 @@ def host():
     L.lp_host_dnrm2.restype = ctypes.c_double
     L.lp_host_dnrm2.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
     L.lp_host_svd_blocks.argtypes = [ctypes.c_void_p, ctypes.c_longlong, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
-                                     ctypes.c_void_p, ctypes.c_int]
+                                     ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
     return L
 
 
@@ -51,20 +51,23 @@ def test_x87_dnrm2_emulation(host):
                 assert np.float64(a).view(np.uint64) == np.float64(b).view(np.uint64), (n, inc)
 
 
+@pytest.mark.parametrize("reverse", [0, 1])
 @pytest.mark.parametrize("b", [4, 6, 8, 10, 12, 14, 16])
-def test_device_route_equals_oracle_route(host, b):
+def test_device_route_equals_oracle_route(host, b, reverse):
+    """reverse=1 runs every per-element loop backwards: the wave-parallel form of the route
+    (one element per lane) is only valid if no element's result depends on another's."""
     from test_oracle_lapack import KINDS, _cover_blocks
 
     for kind in KINDS:
         D = _cover_blocks(kind, b)
         nb = len(D)
         U, Vt, S = np.empty_like(D), np.empty_like(D), np.empty((nb, b), np.float32)
-        assert host.lp_host_svd_blocks(_p(D), nb, b, _p(U), _p(S), _p(Vt), 1) == 0
+        assert host.lp_host_svd_blocks(_p(D), nb, b, _p(U), _p(S), _p(Vt), 1, reverse) == 0
         u, s, vt = O.lp_svd_blocks(D)
         for x, y in ((U, u), (S, s), (Vt, vt)):
             assert np.array_equal(x.view(np.uint32), y.view(np.uint32)), (b, kind)
         S2 = np.empty((nb, b), np.float32)
-        assert host.lp_host_svd_blocks(_p(D), nb, b, None, _p(S2), None, 0) == 0
+        assert host.lp_host_svd_blocks(_p(D), nb, b, None, _p(S2), None, 0, reverse) == 0
         assert np.array_equal(S2.view(np.uint32), s.view(np.uint32)), (b, kind)
 
 

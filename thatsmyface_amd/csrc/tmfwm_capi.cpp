@@ -56,7 +56,50 @@ int check_device_ptr(const void *p, const char *name)
     return 0;
 }
 
-// Device scratch for the host-memory path, released in the destructor.
+// The library's own stream-ordered pool per device (never the device's default pool, which
+// torch's allocator and other libraries share): freed blocks stay cached up to kPoolKeep
+// bytes -- enough for the per-call dgesdd lists and the host path's staging of an app-sized
+// call -- and anything above is returned to the device at the next synchronisation.
+constexpr uint64_t kPoolKeep = uint64_t(1) << 30;
+
+hipMemPool_t lib_pool(int dev)
+{
+    static std::mutex mu;
+    static std::vector<std::pair<int, hipMemPool_t>> pools;
+    std::lock_guard<std::mutex> lk(mu);
+    for (auto &p : pools)
+        if (p.first == dev) return p.second;
+    hipMemPoolProps props{};
+    props.allocType = hipMemAllocationTypePinned;
+    props.handleTypes = hipMemHandleTypeNone;
+    props.location.type = hipMemLocationTypeDevice;
+    props.location.id = dev;
+    hipMemPool_t pool = nullptr;
+    if (hipMemPoolCreate(&pool, &props) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    uint64_t keep = kPoolKeep;
+    (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+    pools.emplace_back(dev, pool);
+    return pool;
+}
+
+// the device a stream belongs to (the null / per-thread stream: the current device)
+int stream_device(hipStream_t st)
+{
+    int dev = 0;
+    if (st != nullptr && st != hipStreamPerThread) {
+        hipDevice_t d = 0;
+        if (hipStreamGetDevice(st, &d) == hipSuccess) return (int)d;
+        (void)hipGetLastError();
+    }
+    if (hipGetDevice(&dev) != hipSuccess) (void)hipGetLastError();
+    return dev;
+}
+
+// Device scratch for one call, stream-ordered from the library's pool on the stream's
+// device, released (stream-ordered) in the destructor.
 struct DevBuf {
     void *p = nullptr;
     hipStream_t st = nullptr;
@@ -68,7 +111,8 @@ struct DevBuf {
     {
         st = s;
         if (n == 0) return 0;
-        hipError_t e = hipMallocAsync(&p, n, s);
+        hipMemPool_t pool = lib_pool(stream_device(s));
+        hipError_t e = pool ? hipMallocFromPoolAsync(&p, n, pool, s) : hipMallocAsync(&p, n, s);
         if (e != hipSuccess) {
             p = nullptr;
             (void)hipGetLastError();
@@ -106,27 +150,6 @@ bool ranges_overlap(const void *a, size_t na, const void *b, size_t nb)
 
 size_t span_bytes(int64_t n, int64_t stride, int64_t frame_bytes) { return n == 0 ? 0 : (size_t)((n - 1) * stride + frame_bytes); }
 
-// The per-call workspaces below come from the device's stream-ordered pool; keep freed
-// memory in the pool instead of returning it at every synchronisation (once per device).
-void keep_pool_memory(hipStream_t st)
-{
-    static std::mutex mu;
-    static std::vector<int> done;
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) { (void)hipGetLastError(); return; }
-    (void)st;
-    std::lock_guard<std::mutex> lk(mu);
-    for (int d : done)
-        if (d == dev) return;
-    hipMemPool_t pool;
-    if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
-        uint64_t keep = UINT64_MAX;
-        (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
-    }
-    (void)hipGetLastError();
-    done.push_back(dev);
-}
-
 // Second-pass bookkeeping: frames go in chunks of at most kListCap
 // blocks (and 65535 frames, the grid's y limit); each chunk's first pass appends the
 // blocks that need the dgesdd route to one shared id list (u32, chunk-relative) and
@@ -160,18 +183,25 @@ struct Chunks {
     }
 };
 
-// copy the per-chunk counts back (synchronises the stream) and sum them
+// copy the per-chunk counts back (synchronises the stream) and sum them; dcounts holds the
+// chunks' dgesdd-route counts, then their non-convergence counts
 int sum_counts(const uint32_t *dcounts, int64_t nchunks, hipStream_t st, int64_t *out)
 {
-    std::vector<uint32_t> h((size_t)nchunks);
+    std::vector<uint32_t> h((size_t)(2 * nchunks));
     if (nchunks) {
-        hipError_t e = hipMemcpyAsync(h.data(), dcounts, (size_t)nchunks * 4, hipMemcpyDeviceToHost, st);
+        hipError_t e = hipMemcpyAsync(h.data(), dcounts, (size_t)nchunks * 8, hipMemcpyDeviceToHost, st);
         if (e == hipSuccess) e = hipStreamSynchronize(st);
         if (e != hipSuccess) return fail(TMFWM_ERR_HIP, "reading the dgesdd-route counts failed: %s", hipGetErrorString(e));
     }
-    int64_t t = 0;
-    for (uint32_t v : h) t += v;
+    int64_t t = 0, bad = 0;
+    for (int64_t c = 0; c < nchunks; ++c) {
+        t += h[(size_t)c];
+        bad += h[(size_t)(nchunks + c)];
+    }
     *out = t;
+    if (bad)
+        return fail(TMFWM_ERR_HIP, "dgesdd route: dbdsqr did not converge on %lld block(s) (np.linalg.svd raises LinAlgError there)",
+                    (long long)bad);
     return 0;
 }
 
@@ -200,10 +230,9 @@ int run_embed(EmbedArgs a, hipStream_t st, int64_t *n_lapack)
     ch.plan(a.nframes, (int64_t)a.nbh * a.nbw);
     DevBuf list, counts;
     if (ch.cap > 0) {
-        keep_pool_memory(st);
         if (int rc = list.alloc((size_t)ch.cap * 4, st, "dgesdd-route block list")) return rc;
-        if (int rc = counts.alloc((size_t)ch.n * 4, st, "dgesdd-route counts")) return rc;
-        TMF_HIP(hipMemsetAsync(counts.p, 0, (size_t)ch.n * 4, st));
+        if (int rc = counts.alloc((size_t)ch.n * 8, st, "dgesdd-route counts")) return rc;
+        TMF_HIP(hipMemsetAsync(counts.p, 0, (size_t)ch.n * 8, st));
     }
     if (ch.cap == 0) {  // no full block: colour round trip only
         TMF_HIP(launch_embed(a, st));
@@ -218,6 +247,7 @@ int run_embed(EmbedArgs a, hipStream_t st, int64_t *n_lapack)
         k.dst = a.dst + f0 * a.frame_stride;
         k.fb_list = static_cast<uint32_t *>(list.p);
         k.fb_count = static_cast<uint32_t *>(counts.p) + c;
+        k.fb_bad = static_cast<uint32_t *>(counts.p) + ch.n + c;
         TMF_HIP(launch_embed(k, st));
         TMF_HIP(launch_embed_fixup(k, k.fb_list, k.fb_count, k.nframes * ch.per_frame, st));
     }
@@ -233,11 +263,10 @@ int run_extract(ExtractArgs a, hipStream_t st, int64_t *n_lapack)
         if (n_lapack) *n_lapack = 0;
         return 0;
     }
-    keep_pool_memory(st);
     DevBuf list, counts;
     if (int rc = list.alloc((size_t)ch.cap * 4, st, "dgesdd-route block list")) return rc;
-    if (int rc = counts.alloc((size_t)ch.n * 4, st, "dgesdd-route counts")) return rc;
-    TMF_HIP(hipMemsetAsync(counts.p, 0, (size_t)ch.n * 4, st));
+    if (int rc = counts.alloc((size_t)ch.n * 8, st, "dgesdd-route counts")) return rc;
+    TMF_HIP(hipMemsetAsync(counts.p, 0, (size_t)ch.n * 8, st));
     for (int64_t c = 0; c < ch.n; ++c) {
         ExtractArgs k = a;
         const int64_t f0 = c * ch.frames;
@@ -247,6 +276,7 @@ int run_extract(ExtractArgs a, hipStream_t st, int64_t *n_lapack)
         k.out = a.out + f0 * a.tile_stride;
         k.fb_list = static_cast<uint32_t *>(list.p);
         k.fb_count = static_cast<uint32_t *>(counts.p) + c;
+        k.fb_bad = static_cast<uint32_t *>(counts.p) + ch.n + c;
         TMF_HIP(launch_extract(k, st));
         TMF_HIP(launch_extract_fixup(k, k.fb_list, k.fb_count, k.nframes * ch.per_frame, st));
     }

@@ -6,26 +6,6 @@
 
 namespace tmf {
 
-hipStream_t aux_stream()
-{
-    static std::mutex mu;
-    static hipStream_t streams[64] = {};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-    std::lock_guard<std::mutex> lk(mu);
-    if (!streams[dev] && hipStreamCreateWithFlags(&streams[dev], hipStreamNonBlocking) != hipSuccess) streams[dev] = nullptr;
-    return streams[dev];
-}
-
-bool fixup_lead_disabled()
-{
-    static const bool off = [] {
-        const char *e = std::getenv("TMFWM_DEBUG_NO_LEAD");
-        return e && *e && *e != '0';
-    }();
-    return off;
-}
-
 #define TMF_FIXUP_DECL(B)                                                                                                    \
     hipError_t launch_embed_fixup_##B(const EmbedArgs &, const uint32_t *, const uint32_t *, int64_t, hipStream_t);          \
     hipError_t launch_extract_fixup_##B(const ExtractArgs &, const uint32_t *, const uint32_t *, int64_t, hipStream_t);
@@ -65,17 +45,20 @@ hipError_t launch_extract_fixup(const ExtractArgs &a, const uint32_t *list, cons
     }
 }
 
-// stage entry points (tmfwm_lapack_svd_blocks, tmfwm_lapack_nrm2)
+// stage entry points (tmfwm_lapack_svd_blocks, tmfwm_lapack_nrm2): the same wave-parallel
+// route as the fixup passes, one 64-lane workgroup per block, the workspace in LDS
 __global__ __launch_bounds__(64) void lp_svd_blocks_kernel(const float *__restrict__ D, int64_t nb, int b, float *__restrict__ U,
                                                            float *__restrict__ S, float *__restrict__ Vt, int want_v,
                                                            int32_t *__restrict__ info)
 {
-    const int64_t k = (int64_t)blockIdx.x * 64 + threadIdx.x;
-    if (k >= nb) return;
-    const int64_t o = k * b * b;
-    const int rc = want_v ? lp::svd_f32<true>(D + o, b, U + o, S + k * b, Vt + o)
-                          : lp::svd_f32<false>(D + o, b, nullptr, S + k * b, nullptr);
-    if (info) info[k] = rc;
+    __shared__ double ws[lp::ws_doubles(lp::kMaxN)];
+    for (int64_t k = blockIdx.x; k < nb; k += gridDim.x) {
+        const int64_t o = k * b * b;
+        const int rc = want_v ? lp::svd_f32_ws<true, lp::WavePar>(D + o, b, U + o, S + k * b, Vt + o, ws)
+                              : lp::svd_f32_ws<false, lp::WavePar>(D + o, b, nullptr, S + k * b, nullptr, ws);
+        if (info && threadIdx.x == 0) info[k] = rc;
+        __syncthreads();
+    }
 }
 
 __global__ __launch_bounds__(64) void lp_nrm2_kernel(const double *__restrict__ x, int64_t nvec, int n, int inc, double *__restrict__ out)
@@ -88,7 +71,7 @@ hipError_t launch_lapack_svd_blocks(const float *D, int64_t nb, int block, float
                                     hipStream_t st)
 {
     if (nb == 0) return hipSuccess;
-    hipLaunchKernelGGL(lp_svd_blocks_kernel, dim3((unsigned)((nb + 63) / 64)), dim3(64), 0, st, D, nb, block, U, S, Vt, want_v, info);
+    hipLaunchKernelGGL(lp_svd_blocks_kernel, dim3((unsigned)(nb < 16384 ? nb : 16384)), dim3(64), 0, st, D, nb, block, U, S, Vt, want_v, info);
     return hipGetLastError();
 }
 

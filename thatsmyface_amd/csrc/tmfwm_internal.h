@@ -20,6 +20,7 @@ struct EmbedArgs {
     // relative to this launch, appended at fb_list[atomicAdd(fb_count, 1)]
     uint32_t *fb_list;
     uint32_t *fb_count;
+    uint32_t *fb_bad;        // dgesdd-route blocks whose dbdsqr did not converge (may be null)
 };
 
 struct ExtractArgs {
@@ -34,6 +35,7 @@ struct ExtractArgs {
     float alpha32;           // f32(alpha): numpy-2 weak-scalar promotion (watermarking.py:285)
     uint32_t *fb_list;       // blocks whose sigma_1 enclosure is undecided (dgesdd route)
     uint32_t *fb_count;
+    uint32_t *fb_bad;        // dgesdd-route blocks whose dbdsqr did not converge (may be null)
 };
 
 struct EdgeArgs {

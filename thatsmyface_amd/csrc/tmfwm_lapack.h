@@ -14,9 +14,17 @@
 // accumulators, fsqrt, then a second rounding to double -- emulated here in integer
 // arithmetic (X80).
 //
-// This is the slow, exact path: one thread per block, matrices in private memory.  The
-// fused kernels take it only for the blocks the conditioning test sends to it (embed)
-// or whose sigma_1 enclosure does not decide the f32 value (extract).
+// Every routine is written over a lane policy P (below): SerialPar runs it on one thread
+// (the host build of the CPU tests); WavePar runs one block per 64-lane wave (the fixup
+// kernels and the stage entry point).  Under WavePar the scalar parts (dnrm2, dlartg,
+// dlasv2, the dbdsqr recurrences, the scans) run uniformly on every lane, and the loops
+// over matrix elements -- dgemv columns / rows, dger and the scalings' elements, drot /
+// dlasr / dswap positions -- are spread over the lanes (LP_PAR): each element gets the
+// same operations in the same order as on one thread, so the bits do not depend on the
+// policy.  A loop body touches only its own element(s); P::sync() (a workgroup barrier:
+// the workgroup is the one wave) orders a loop's stores before other lanes' loads.
+// The fused kernels take this route only for the blocks the conditioning test sends to
+// it (embed) or whose sigma_1 enclosure does not decide the f32 value (extract).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -26,8 +34,12 @@ namespace lp {
 
 // host + device: the CPU test suite compiles this same code for the host
 // (tests/native/lp_host.cpp) and checks it against the oracle before any GPU run
+// Every routine is inlined: on the GPU a call saves and restores callee-saved registers
+// through scratch (global memory), and the route makes hundreds of calls per block -- as
+// noinline functions they cost ~1 ms per block (profiles/r03/r03d_*); the working arrays
+// are in the caller's LDS workspace, so inlining adds no private memory.
 #define TMF_LPI __host__ __device__ inline __attribute__((always_inline))
-#define TMF_LPN __host__ __device__ inline __attribute__((noinline))  // inline: one definition per TU is fine (tmfwm_fixup<b>.hip)
+#define TMF_LPN TMF_LPI
 
 constexpr int kMaxN = 16;
 constexpr double kEps = 0x1p-53;                     // dlamch('E')
@@ -37,6 +49,71 @@ constexpr double kHuge = 0x1.fffffffffffffp+1023;    // dlamch('O')
 constexpr double kTolmul = 0x1.8ace5422aa0dbp+6;     // max(10, min(100, eps**-0.125)) (glibc pow, pinned by a CPU test)
 constexpr double kRtmax = 0x1.6a09e667f3bcdp+510;    // sqrt(safmax / 2) in dlartg
 constexpr double kRtmin = 0x1p-511;                  // sqrt(safmin)
+
+// ---------------------------------------------------------------------------
+// lane policies
+// ---------------------------------------------------------------------------
+struct SerialPar {
+    TMF_LPI static int lane() { return 0; }
+    static constexpr int kLanes = 1;
+    TMF_LPI static void sync() {}
+};
+// the same loops run backwards (host tests: element bodies must not depend on the order)
+struct ReversePar {
+    static constexpr int kLanes = 1;
+    static constexpr bool kReverse = true;
+    TMF_LPI static void sync() {}
+};
+struct WavePar {  // device code only
+    __device__ __forceinline__ static int lane() { return (int)(threadIdx.x & 63u); }
+    static constexpr int kLanes = 64;
+    __device__ __forceinline__ static void sync() { __syncthreads(); }  // workgroup == one wave
+};
+template <class P, class = void>
+struct IsReverse { static constexpr bool v = false; };
+template <class P>
+struct IsReverse<P, decltype((void)P::kReverse)> { static constexpr bool v = P::kReverse; };
+
+// for (int K = first; K < N; K += step) over this lane's share of [0, N)
+#define LP_PAR(P, K, N)                                                                                     \
+    for (int K##_n = (N), K##_i = IsReverse<P>::v ? K##_n - 1 : lane_of<P>(); IsReverse<P>::v ? K##_i >= 0 : K##_i < K##_n; \
+         K##_i += IsReverse<P>::v ? -1 : P::kLanes)                                                          \
+        if (const int K = K##_i; true)
+template <class P>
+TMF_LPI int lane_of()
+{
+    if constexpr (IsReverse<P>::v) return 0;
+    else return P::lane();
+}
+
+// A vector of <= 16 doubles that every lane reads and writes alike (dbdsqr's d, e and its
+// rotation sequences): a plain array on one thread; under WavePar element i lives in lane
+// i's register and is read with readlane (its index is uniform), written with a lane
+// select -- the scalar recurrences then wait on register moves, not on LDS round trips.
+template <class P>
+struct LVec {
+    double v[kMaxN];
+    TMF_LPI double get(int i) const { return v[i]; }
+    TMF_LPI void set(int i, double x) { v[i] = x; }
+    TMF_LPI void load(const double *src, int n) { for (int i = 0; i < n; ++i) v[i] = src[i]; }
+    TMF_LPI void store_f32(float *dst, int n) const { for (int i = 0; i < n; ++i) dst[i] = (float)v[i]; }
+};
+template <>
+struct LVec<WavePar> {
+    double v = 0.0;
+    __device__ __forceinline__ double get(int i) const
+    {
+        const long long b = __builtin_bit_cast(long long, v);
+        const int lo = __builtin_amdgcn_readlane((int)b, i), hi = __builtin_amdgcn_readlane((int)(b >> 32), i);
+        return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+    }
+    __device__ __forceinline__ void set(int i, double x) { v = WavePar::lane() == i ? x : v; }
+    __device__ __forceinline__ void load(const double *src, int n) { v = WavePar::lane() < n ? src[WavePar::lane()] : 0.0; }
+    __device__ __forceinline__ void store_f32(float *dst, int n) const
+    {
+        if (WavePar::lane() < n) dst[WavePar::lane()] = (float)v;
+    }
+};
 
 // ---------------------------------------------------------------------------
 // x87 extended arithmetic for dnrm2 (non-negative values only: squares and sums)
@@ -117,13 +194,16 @@ TMF_LPI double x80_sqrt_to_double(X80 t)
     const double nd = (double)(uint64_t)(N >> 64) * 0x1p64 + (double)(uint64_t)N;
     double rd = __builtin_sqrt(nd);
     uint64_t r = rd >= 0x1p64 ? 0xffffffffffffffffull : (uint64_t)rd;
-    // one Newton correction in floating point, then exact integer fix-up
+    // one Newton correction, its step (|step| < ~2^12: rd carries 53 of the 64 bits) rounded in
+    // floating point but applied in integer arithmetic -- applied as r + step in a double, the
+    // sum would lose the low 11 bits again and leave thousands of fix-up iterations below
     {
         const u128 rr = (u128)r * r;
-        const double diff = rr > N ? -(double)(rr - N) : (double)(N - rr);
-        const double delta = diff / (2.0 * (double)r);
-        const double rn = (double)r + __builtin_rint(delta);
-        r = rn >= 0x1p64 ? 0xffffffffffffffffull : (rn < 0x1p63 ? 0x8000000000000000ull : (uint64_t)rn);
+        const bool over = rr > N;
+        const double delta = (double)(over ? rr - N : N - rr) / (2.0 * (double)r);
+        const uint64_t step = (uint64_t)__builtin_rint(delta);
+        if (over) r = step > r - 0x8000000000000000ull ? 0x8000000000000000ull : r - step;
+        else r = step > 0xffffffffffffffffull - r ? 0xffffffffffffffffull : r + step;
     }
     while ((u128)r * r > N) --r;
     while (r != 0xffffffffffffffffull && (u128)(r + 1) * (r + 1) <= N) ++r;
@@ -172,10 +252,11 @@ TMF_LPN double dnrm2(int n, const double *x, int inc)
 // ---------------------------------------------------------------------------
 #define LP_AT(a, i, j, ld) (a)[(i) + (j) * (ld)]
 
+template <class P>
 TMF_LPN void gemv_t(int m, int n, const double *A, int lda, const double *x, int incx, double *y)
 {
     const int m3 = m & 3, m1 = m - m3, n4 = n & ~3, n2 = n & 3;
-    for (int j = 0; j < n; ++j) {
+    LP_PAR(P, j, n) {
         const double *a = A + j * lda;
         double yy = 0.0;
         if (m1) {
@@ -217,62 +298,73 @@ TMF_LPN void gemv_t(int m, int n, const double *A, int lda, const double *x, int
             yy = __builtin_fma(a[m1], xt[0], yy);
         y[j] = yy;
     }
+    P::sync();
 }
 
+template <class P>
 TMF_LPN void gemv_n(int m, int n, const double *A, int lda, const double *x, int incx, double *y)
 {
     const int m3 = m & 3, m1 = m - m3, n4 = n & ~3;
-    for (int r = 0; r < m1; ++r) {
-        double yr = 0.0;
-        int j = 0;
-        for (; j < n4; j += 4) {
-            double s = LP_AT(A, r, j + 1, lda) * x[(j + 1) * incx];
-            s = __builtin_fma(LP_AT(A, r, j, lda), x[j * incx], s);
-            s = __builtin_fma(LP_AT(A, r, j + 2, lda), x[(j + 2) * incx], s);
-            s = __builtin_fma(LP_AT(A, r, j + 3, lda), x[(j + 3) * incx], s);
-            yr = __builtin_fma(1.0, s, yr);
+    LP_PAR(P, r, m) {
+        if (r < m1) {
+            double yr = 0.0;
+            int j = 0;
+            for (; j < n4; j += 4) {
+                double s = LP_AT(A, r, j + 1, lda) * x[(j + 1) * incx];
+                s = __builtin_fma(LP_AT(A, r, j, lda), x[j * incx], s);
+                s = __builtin_fma(LP_AT(A, r, j + 2, lda), x[(j + 2) * incx], s);
+                s = __builtin_fma(LP_AT(A, r, j + 3, lda), x[(j + 3) * incx], s);
+                yr = __builtin_fma(1.0, s, yr);
+            }
+            if (incx == 1 && (n & 2)) {
+                double s = LP_AT(A, r, j + 1, lda) * x[j + 1];
+                s = __builtin_fma(LP_AT(A, r, j, lda), x[j], s);
+                yr = __builtin_fma(1.0, s, yr);
+                j += 2;
+            }
+            for (; j < n; ++j) yr = yr + LP_AT(A, r, j, lda) * (x[j * incx] * 1.0);
+            y[r] = yr;
+        } else {
+            double t = 0.0;
+            for (int j = 0; j < n; ++j) t = __builtin_fma(LP_AT(A, r, j, lda), x[j * incx], t);
+            y[r] = __builtin_fma(1.0, t, 0.0);
         }
-        if (incx == 1 && (n & 2)) {
-            double s = LP_AT(A, r, j + 1, lda) * x[j + 1];
-            s = __builtin_fma(LP_AT(A, r, j, lda), x[j], s);
-            yr = __builtin_fma(1.0, s, yr);
-            j += 2;
-        }
-        for (; j < n; ++j) yr = yr + LP_AT(A, r, j, lda) * (x[j * incx] * 1.0);
-        y[r] = yr;
     }
-    for (int r = m1; r < m; ++r) {
-        double t = 0.0;
-        for (int j = 0; j < n; ++j) t = __builtin_fma(LP_AT(A, r, j, lda), x[j * incx], t);
-        y[r] = __builtin_fma(1.0, t, 0.0);
-    }
+    P::sync();
 }
 
+template <class P>
 TMF_LPI void ger(int m, int n, double alpha, const double *x, int incx, const double *y, int incy, double *A, int lda)
 {
     if (m <= 0 || n <= 0 || alpha == 0.0) return;
-    for (int j = 0; j < n; ++j) {
+    LP_PAR(P, k, m * n) {
+        const int j = k / m, i = k - j * m;
         const double t = alpha * y[j * incy];
-        for (int i = 0; i < m; ++i) LP_AT(A, i, j, lda) = __builtin_fma(t, x[i * incx], LP_AT(A, i, j, lda));
+        LP_AT(A, i, j, lda) = __builtin_fma(t, x[i * incx], LP_AT(A, i, j, lda));
     }
+    P::sync();
 }
 
+template <class P>
 TMF_LPI void drot(int n, double *x, int incx, double *y, int incy, double c, double s)
 {
-    for (int i = 0; i < n; ++i) {
+    LP_PAR(P, i, n) {
         const double xi = x[i * incx], yi = y[i * incy];
         x[i * incx] = __builtin_fma(c, xi, s * yi);
         y[i * incy] = __builtin_fma(c, yi, -(s * xi));
     }
+    P::sync();
 }
 
+template <class P>
 TMF_LPI void dswap(int n, double *x, int incx, double *y, int incy)
 {
-    for (int i = 0; i < n; ++i) {
+    LP_PAR(P, i, n) {
         const double t = x[i * incx];
         x[i * incx] = y[i * incy];
         y[i * incy] = t;
     }
+    P::sync();
 }
 
 // ---------------------------------------------------------------------------
@@ -291,8 +383,10 @@ TMF_LPI double dlapy2(double x, double y)
     return w * __builtin_sqrt(1.0 + q * q);
 }
 
+template <class P>
 TMF_LPN void dlarfg(int n, double *alpha, double *x, int incx, double *tau)
 {
+    // scalars (*alpha, *tau, beta, the norms) are computed, read and written by every lane alike
     if (n <= 1) { *tau = 0.0; return; }
     double xnorm = dnrm2(n - 1, x, incx);
     if (xnorm == 0.0) { *tau = 0.0; return; }
@@ -302,7 +396,8 @@ TMF_LPN void dlarfg(int n, double *alpha, double *x, int incx, double *tau)
     if (__builtin_fabs(beta) < safmin) {
         do {
             ++knt;
-            for (int i = 0; i < n - 1; ++i) x[i * incx] *= rsafmn;
+            LP_PAR(P, i, n - 1) x[i * incx] *= rsafmn;
+            P::sync();
             beta *= rsafmn;
             *alpha *= rsafmn;
         } while (__builtin_fabs(beta) < safmin && knt < 20);
@@ -311,7 +406,8 @@ TMF_LPN void dlarfg(int n, double *alpha, double *x, int incx, double *tau)
     }
     *tau = (beta - *alpha) / beta;
     const double sc = 1.0 / (*alpha - beta);
-    for (int i = 0; i < n - 1; ++i) x[i * incx] *= sc;
+    LP_PAR(P, i, n - 1) x[i * incx] *= sc;
+    P::sync();
     for (int j = 0; j < knt; ++j) beta *= safmin;
     *alpha = beta;
 }
@@ -339,6 +435,7 @@ TMF_LPI int iladlr(int m, int n, const double *A, int lda)
     return r;
 }
 
+template <class P>
 TMF_LPN void dlarf(int left, int m, int n, const double *v, int incv, double tau, double *C, int ldc, double *work)
 {
     int lastv = 0, lastc = 0;
@@ -350,28 +447,29 @@ TMF_LPN void dlarf(int left, int m, int n, const double *v, int incv, double tau
     }
     if (lastv <= 0 || lastc <= 0) return;
     if (left) {
-        gemv_t(lastv, lastc, C, ldc, v, incv, work);
-        ger(lastv, lastc, -tau, v, incv, work, 1, C, ldc);
+        gemv_t<P>(lastv, lastc, C, ldc, v, incv, work);
+        ger<P>(lastv, lastc, -tau, v, incv, work, 1, C, ldc);
     } else {
-        gemv_n(lastc, lastv, C, ldc, v, incv, work);
-        ger(lastc, lastv, -tau, work, 1, v, incv, C, ldc);
+        gemv_n<P>(lastc, lastv, C, ldc, v, incv, work);
+        ger<P>(lastc, lastv, -tau, work, 1, v, incv, C, ldc);
     }
 }
 
+template <class P>
 TMF_LPN void dgebd2(int n, double *A, int lda, double *d, double *e, double *tauq, double *taup, double *work)
 {
     const int m = n;
     for (int i = 0; i < n; ++i) {
-        dlarfg(m - i, &LP_AT(A, i, i, lda), &LP_AT(A, (i + 1 < m ? i + 1 : m - 1), i, lda), 1, &tauq[i]);
+        dlarfg<P>(m - i, &LP_AT(A, i, i, lda), &LP_AT(A, (i + 1 < m ? i + 1 : m - 1), i, lda), 1, &tauq[i]);
         d[i] = LP_AT(A, i, i, lda);
         LP_AT(A, i, i, lda) = 1.0;
-        if (i < n - 1) dlarf(1, m - i, n - i - 1, &LP_AT(A, i, i, lda), 1, tauq[i], &LP_AT(A, i, i + 1, lda), lda, work);
+        if (i < n - 1) dlarf<P>(1, m - i, n - i - 1, &LP_AT(A, i, i, lda), 1, tauq[i], &LP_AT(A, i, i + 1, lda), lda, work);
         LP_AT(A, i, i, lda) = d[i];
         if (i < n - 1) {
-            dlarfg(n - i - 1, &LP_AT(A, i, i + 1, lda), &LP_AT(A, i, (i + 2 < n ? i + 2 : n - 1), lda), lda, &taup[i]);
+            dlarfg<P>(n - i - 1, &LP_AT(A, i, i + 1, lda), &LP_AT(A, i, (i + 2 < n ? i + 2 : n - 1), lda), lda, &taup[i]);
             e[i] = LP_AT(A, i, i + 1, lda);
             LP_AT(A, i, i + 1, lda) = 1.0;
-            dlarf(0, m - i - 1, n - i - 1, &LP_AT(A, i, i + 1, lda), lda, taup[i], &LP_AT(A, i + 1, i + 1, lda), lda, work);
+            dlarf<P>(0, m - i - 1, n - i - 1, &LP_AT(A, i, i + 1, lda), lda, taup[i], &LP_AT(A, i + 1, i + 1, lda), lda, work);
             LP_AT(A, i, i + 1, lda) = e[i];
         } else {
             taup[i] = 0.0;
@@ -504,51 +602,53 @@ TMF_LPN void dlasv2(double f, double g, double h, double *ssmin, double *ssmax, 
     *ssmin = fsign(*ssmin, tsign * fsign(1.0, f) * fsign(1.0, h));
 }
 
-// dlasr, PIVOT = 'V': left -> rows j, j+1 of an m x n A; right -> columns j, j+1
-TMF_LPN void dlasr(bool left, bool fwd, int m, int n, const double *c, const double *s, double *A, int lda)
+// dlasr, PIVOT = 'V': left -> rows j, j+1 of an m x n A; right -> columns j, j+1; the
+// rotations (c, s) are elements [0, k-1) of two LVecs.  A lane keeps one column (left) /
+// row (right) through every rotation of the sequence.
+template <class P>
+TMF_LPN void dlasr(bool left, bool fwd, int m, int n, const LVec<P> &c, const LVec<P> &s, double *A, int lda)
 {
     const int k = left ? m : n;
-    for (int q = 0; q < k - 1; ++q) {
-        const int j = fwd ? q : k - 2 - q;
-        const double ct = c[j], st = s[j];
-        if (ct == 1.0 && st == 0.0) continue;
-        if (left) {
-            for (int i = 0; i < n; ++i) {
+    LP_PAR(P, i, left ? n : m) {
+        for (int q = 0; q < k - 1; ++q) {
+            const int j = fwd ? q : k - 2 - q;
+            const double ct = c.get(j), st = s.get(j);
+            if (ct == 1.0 && st == 0.0) continue;
+            if (left) {
                 const double t = LP_AT(A, j + 1, i, lda);
                 LP_AT(A, j + 1, i, lda) = ct * t - st * LP_AT(A, j, i, lda);
                 LP_AT(A, j, i, lda) = st * t + ct * LP_AT(A, j, i, lda);
-            }
-        } else {
-            for (int i = 0; i < m; ++i) {
+            } else {
                 const double t = LP_AT(A, i, j + 1, lda);
                 LP_AT(A, i, j + 1, lda) = ct * t - st * LP_AT(A, i, j, lda);
                 LP_AT(A, i, j, lda) = st * t + ct * LP_AT(A, i, j, lda);
             }
         }
     }
+    P::sync();
 }
 
 // dbdsqr('U', n, ncvt = n, nru = n, ncc = 0).  WANT_V = false skips the vector
 // updates only (the d / e recurrences do not read the vectors, so the singular values
 // are those of the vector-carrying run -- not dlasq1's, which LAPACK would use without
 // vectors and numpy never does).  Returns 0, or 1 if not converged.
-template <bool WANT_V>
-TMF_LPN int dbdsqr(int n, double *d, double *e, double *VT, int ldvt, double *U, int ldu, double *work)
+template <bool WANT_V, class P>
+TMF_LPN int dbdsqr(int n, LVec<P> &d, LVec<P> &e, double *VT, int ldvt, double *U, int ldu)
 {
     const int maxitr = 6;
     if (n == 0) return 0;
     if (n > 1) {
-        const int nm1 = n - 1, nm12 = nm1 + nm1, nm13 = nm12 + nm1;
+        LVec<P> w0, w1, w2, w3;  // LAPACK's WORK(1..4(n-1)) as its four (n-1)-long sequences
         const double eps = kEps, unfl = kSafmin;
         const double tol = kTolmul * eps;
         double smax = 0.0;
-        for (int i = 0; i < n; ++i) smax = dmax(smax, __builtin_fabs(d[i]));
-        for (int i = 0; i < n - 1; ++i) smax = dmax(smax, __builtin_fabs(e[i]));
-        double sminoa = __builtin_fabs(d[0]);
+        for (int i = 0; i < n; ++i) smax = dmax(smax, __builtin_fabs(d.get(i)));
+        for (int i = 0; i < n - 1; ++i) smax = dmax(smax, __builtin_fabs(e.get(i)));
+        double sminoa = __builtin_fabs(d.get(0));
         if (sminoa != 0.0) {
             double mu = sminoa;
             for (int i = 1; i < n; ++i) {
-                mu = __builtin_fabs(d[i]) * (mu / (mu + __builtin_fabs(e[i - 1])));
+                mu = __builtin_fabs(d.get(i)) * (mu / (mu + __builtin_fabs(e.get(i - 1))));
                 sminoa = dmin(sminoa, mu);
                 if (sminoa == 0.0) break;
             }
@@ -562,9 +662,8 @@ TMF_LPN int dbdsqr(int n, double *d, double *e, double *VT, int ldvt, double *U,
         const int maxitdivn = maxitr * n;
         int iterdivn = 0, iter = -1, oldll = -1, oldm = -1, idir = 0;
         int m = n;
-#define D_(i) d[(i) - 1]
-#define E_(i) e[(i) - 1]
-#define W_(i) work[(i) - 1]
+#define D_(i) d.get((i) - 1)
+#define E_(i) e.get((i) - 1)
         for (;;) {
             if (m <= 1) break;
             if (iter >= n) {
@@ -583,7 +682,7 @@ TMF_LPN int dbdsqr(int n, double *d, double *e, double *VT, int ldvt, double *U,
                 smax = dmax(smax, dmax(abss, abse));
             }
             if (split) {
-                E_(ll) = 0.0;
+                e.set((ll) - 1, 0.0);
                 if (ll == m - 1) { m = m - 1; continue; }
             } else {
                 ll = 0;
@@ -592,12 +691,12 @@ TMF_LPN int dbdsqr(int n, double *d, double *e, double *VT, int ldvt, double *U,
             if (ll == m - 1) {
                 double sigmn, sigmx, sinr, cosr, sinl, cosl;
                 dlasv2(D_(m - 1), E_(m - 1), D_(m), &sigmn, &sigmx, &sinr, &cosr, &sinl, &cosl);
-                D_(m - 1) = sigmx;
-                E_(m - 1) = 0.0;
-                D_(m) = sigmn;
+                d.set((m - 1) - 1, sigmx);
+                e.set((m - 1) - 1, 0.0);
+                d.set((m) - 1, sigmn);
                 if (WANT_V) {
-                    drot(n, &LP_AT(VT, m - 2, 0, ldvt), ldvt, &LP_AT(VT, m - 1, 0, ldvt), ldvt, cosr, sinr);
-                    drot(n, &LP_AT(U, 0, m - 2, ldu), 1, &LP_AT(U, 0, m - 1, ldu), 1, cosl, sinl);
+                    drot<P>(n, &LP_AT(VT, m - 2, 0, ldvt), ldvt, &LP_AT(VT, m - 1, 0, ldvt), ldvt, cosr, sinr);
+                    drot<P>(n, &LP_AT(U, 0, m - 2, ldu), 1, &LP_AT(U, 0, m - 1, ldu), 1, cosl, sinl);
                 }
                 m = m - 2;
                 continue;
@@ -605,20 +704,20 @@ TMF_LPN int dbdsqr(int n, double *d, double *e, double *VT, int ldvt, double *U,
             if (ll > oldm || m < oldll) idir = __builtin_fabs(D_(ll)) >= __builtin_fabs(D_(m)) ? 1 : 2;
             bool conv = false;
             if (idir == 1) {
-                if (__builtin_fabs(E_(m - 1)) <= __builtin_fabs(tol) * __builtin_fabs(D_(m))) { E_(m - 1) = 0.0; continue; }
+                if (__builtin_fabs(E_(m - 1)) <= __builtin_fabs(tol) * __builtin_fabs(D_(m))) { e.set((m - 1) - 1, 0.0); continue; }
                 double mu = __builtin_fabs(D_(ll));
                 smin = mu;
                 for (int lll = ll; lll <= m - 1; ++lll) {
-                    if (__builtin_fabs(E_(lll)) <= tol * mu) { E_(lll) = 0.0; conv = true; break; }
+                    if (__builtin_fabs(E_(lll)) <= tol * mu) { e.set((lll) - 1, 0.0); conv = true; break; }
                     mu = __builtin_fabs(D_(lll + 1)) * (mu / (mu + __builtin_fabs(E_(lll))));
                     smin = dmin(smin, mu);
                 }
             } else {
-                if (__builtin_fabs(E_(ll)) <= __builtin_fabs(tol) * __builtin_fabs(D_(ll))) { E_(ll) = 0.0; continue; }
+                if (__builtin_fabs(E_(ll)) <= __builtin_fabs(tol) * __builtin_fabs(D_(ll))) { e.set((ll) - 1, 0.0); continue; }
                 double mu = __builtin_fabs(D_(m));
                 smin = mu;
                 for (int lll = m - 1; lll >= ll; --lll) {
-                    if (__builtin_fabs(E_(lll)) <= tol * mu) { E_(lll) = 0.0; conv = true; break; }
+                    if (__builtin_fabs(E_(lll)) <= tol * mu) { e.set((lll) - 1, 0.0); conv = true; break; }
                     mu = __builtin_fabs(D_(lll)) * (mu / (mu + __builtin_fabs(E_(lll))));
                     smin = dmin(smin, mu);
                 }
@@ -648,40 +747,40 @@ TMF_LPN int dbdsqr(int n, double *d, double *e, double *VT, int ldvt, double *U,
                     double cs = 1.0, oldcs = 1.0, sn = 0.0, oldsn = 0.0;
                     for (int i = ll; i <= m - 1; ++i) {
                         dlartg(D_(i) * cs, E_(i), &cs, &sn, &r);
-                        if (i > ll) E_(i - 1) = oldsn * r;
-                        dlartg(oldcs * r, D_(i + 1) * sn, &oldcs, &oldsn, &D_(i));
-                        W_(i - ll + 1) = cs;
-                        W_(i - ll + 1 + nm1) = sn;
-                        W_(i - ll + 1 + nm12) = oldcs;
-                        W_(i - ll + 1 + nm13) = oldsn;
+                        if (i > ll) e.set((i - 1) - 1, oldsn * r);
+                        { double di; dlartg(oldcs * r, D_(i + 1) * sn, &oldcs, &oldsn, &di); d.set(i - 1, di); }
+                        w0.set(i - ll, cs);
+                        w1.set(i - ll, sn);
+                        w2.set(i - ll, oldcs);
+                        w3.set(i - ll, oldsn);
                     }
                     const double h = D_(m) * cs;
-                    D_(m) = h * oldcs;
-                    E_(m - 1) = h * oldsn;
+                    d.set((m) - 1, h * oldcs);
+                    e.set((m - 1) - 1, h * oldsn);
                     if (WANT_V) {
-                        dlasr(true, true, m - ll + 1, n, &W_(1), &W_(n), &LP_AT(VT, ll - 1, 0, ldvt), ldvt);
-                        dlasr(false, true, n, m - ll + 1, &W_(nm12 + 1), &W_(nm13 + 1), &LP_AT(U, 0, ll - 1, ldu), ldu);
+                        dlasr<P>(true, true, m - ll + 1, n, w0, w1, &LP_AT(VT, ll - 1, 0, ldvt), ldvt);
+                        dlasr<P>(false, true, n, m - ll + 1, w2, w3, &LP_AT(U, 0, ll - 1, ldu), ldu);
                     }
-                    if (__builtin_fabs(E_(m - 1)) <= thresh) E_(m - 1) = 0.0;
+                    if (__builtin_fabs(E_(m - 1)) <= thresh) e.set((m - 1) - 1, 0.0);
                 } else {
                     double cs = 1.0, oldcs = 1.0, sn = 0.0, oldsn = 0.0;
                     for (int i = m; i >= ll + 1; --i) {
                         dlartg(D_(i) * cs, E_(i - 1), &cs, &sn, &r);
-                        if (i < m) E_(i) = oldsn * r;
-                        dlartg(oldcs * r, D_(i - 1) * sn, &oldcs, &oldsn, &D_(i));
-                        W_(i - ll) = cs;
-                        W_(i - ll + nm1) = -sn;
-                        W_(i - ll + nm12) = oldcs;
-                        W_(i - ll + nm13) = -oldsn;
+                        if (i < m) e.set((i) - 1, oldsn * r);
+                        { double di; dlartg(oldcs * r, D_(i - 1) * sn, &oldcs, &oldsn, &di); d.set(i - 1, di); }
+                        w0.set(i - ll - 1, cs);
+                        w1.set(i - ll - 1, -sn);
+                        w2.set(i - ll - 1, oldcs);
+                        w3.set(i - ll - 1, -oldsn);
                     }
                     const double h = D_(ll) * cs;
-                    D_(ll) = h * oldcs;
-                    E_(ll) = h * oldsn;
+                    d.set((ll) - 1, h * oldcs);
+                    e.set((ll) - 1, h * oldsn);
                     if (WANT_V) {
-                        dlasr(true, false, m - ll + 1, n, &W_(nm12 + 1), &W_(nm13 + 1), &LP_AT(VT, ll - 1, 0, ldvt), ldvt);
-                        dlasr(false, false, n, m - ll + 1, &W_(1), &W_(n), &LP_AT(U, 0, ll - 1, ldu), ldu);
+                        dlasr<P>(true, false, m - ll + 1, n, w2, w3, &LP_AT(VT, ll - 1, 0, ldvt), ldvt);
+                        dlasr<P>(false, false, n, m - ll + 1, w0, w1, &LP_AT(U, 0, ll - 1, ldu), ldu);
                     }
-                    if (__builtin_fabs(E_(ll)) <= thresh) E_(ll) = 0.0;
+                    if (__builtin_fabs(E_(ll)) <= thresh) e.set((ll) - 1, 0.0);
                 }
             } else {
                 if (idir == 1) {
@@ -690,85 +789,86 @@ TMF_LPN int dbdsqr(int n, double *d, double *e, double *VT, int ldvt, double *U,
                     double cosr, sinr, cosl, sinl;
                     for (int i = ll; i <= m - 1; ++i) {
                         dlartg(f, g, &cosr, &sinr, &r);
-                        if (i > ll) E_(i - 1) = r;
+                        if (i > ll) e.set((i - 1) - 1, r);
                         f = cosr * D_(i) + sinr * E_(i);
-                        E_(i) = cosr * E_(i) - sinr * D_(i);
+                        e.set((i) - 1, cosr * E_(i) - sinr * D_(i));
                         g = sinr * D_(i + 1);
-                        D_(i + 1) = cosr * D_(i + 1);
+                        d.set((i + 1) - 1, cosr * D_(i + 1));
                         dlartg(f, g, &cosl, &sinl, &r);
-                        D_(i) = r;
+                        d.set((i) - 1, r);
                         f = cosl * E_(i) + sinl * D_(i + 1);
-                        D_(i + 1) = cosl * D_(i + 1) - sinl * E_(i);
+                        d.set((i + 1) - 1, cosl * D_(i + 1) - sinl * E_(i));
                         if (i < m - 1) {
                             g = sinl * E_(i + 1);
-                            E_(i + 1) = cosl * E_(i + 1);
+                            e.set((i + 1) - 1, cosl * E_(i + 1));
                         }
-                        W_(i - ll + 1) = cosr;
-                        W_(i - ll + 1 + nm1) = sinr;
-                        W_(i - ll + 1 + nm12) = cosl;
-                        W_(i - ll + 1 + nm13) = sinl;
+                        w0.set(i - ll, cosr);
+                        w1.set(i - ll, sinr);
+                        w2.set(i - ll, cosl);
+                        w3.set(i - ll, sinl);
                     }
-                    E_(m - 1) = f;
+                    e.set((m - 1) - 1, f);
                     if (WANT_V) {
-                        dlasr(true, true, m - ll + 1, n, &W_(1), &W_(n), &LP_AT(VT, ll - 1, 0, ldvt), ldvt);
-                        dlasr(false, true, n, m - ll + 1, &W_(nm12 + 1), &W_(nm13 + 1), &LP_AT(U, 0, ll - 1, ldu), ldu);
+                        dlasr<P>(true, true, m - ll + 1, n, w0, w1, &LP_AT(VT, ll - 1, 0, ldvt), ldvt);
+                        dlasr<P>(false, true, n, m - ll + 1, w2, w3, &LP_AT(U, 0, ll - 1, ldu), ldu);
                     }
-                    if (__builtin_fabs(E_(m - 1)) <= thresh) E_(m - 1) = 0.0;
+                    if (__builtin_fabs(E_(m - 1)) <= thresh) e.set((m - 1) - 1, 0.0);
                 } else {
                     double f = (__builtin_fabs(D_(m)) - shift) * (fsign(1.0, D_(m)) + shift / D_(m));
                     double g = E_(m - 1);
                     double cosr, sinr, cosl, sinl;
                     for (int i = m; i >= ll + 1; --i) {
                         dlartg(f, g, &cosr, &sinr, &r);
-                        if (i < m) E_(i) = r;
+                        if (i < m) e.set((i) - 1, r);
                         f = cosr * D_(i) + sinr * E_(i - 1);
-                        E_(i - 1) = cosr * E_(i - 1) - sinr * D_(i);
+                        e.set((i - 1) - 1, cosr * E_(i - 1) - sinr * D_(i));
                         g = sinr * D_(i - 1);
-                        D_(i - 1) = cosr * D_(i - 1);
+                        d.set((i - 1) - 1, cosr * D_(i - 1));
                         dlartg(f, g, &cosl, &sinl, &r);
-                        D_(i) = r;
+                        d.set((i) - 1, r);
                         f = cosl * E_(i - 1) + sinl * D_(i - 1);
-                        D_(i - 1) = cosl * D_(i - 1) - sinl * E_(i - 1);
+                        d.set((i - 1) - 1, cosl * D_(i - 1) - sinl * E_(i - 1));
                         if (i > ll + 1) {
                             g = sinl * E_(i - 2);
-                            E_(i - 2) = cosl * E_(i - 2);
+                            e.set((i - 2) - 1, cosl * E_(i - 2));
                         }
-                        W_(i - ll) = cosr;
-                        W_(i - ll + nm1) = -sinr;
-                        W_(i - ll + nm12) = cosl;
-                        W_(i - ll + nm13) = -sinl;
+                        w0.set(i - ll - 1, cosr);
+                        w1.set(i - ll - 1, -sinr);
+                        w2.set(i - ll - 1, cosl);
+                        w3.set(i - ll - 1, -sinl);
                     }
-                    E_(ll) = f;
-                    if (__builtin_fabs(E_(ll)) <= thresh) E_(ll) = 0.0;
+                    e.set((ll) - 1, f);
+                    if (__builtin_fabs(E_(ll)) <= thresh) e.set((ll) - 1, 0.0);
                     if (WANT_V) {
-                        dlasr(true, false, m - ll + 1, n, &W_(nm12 + 1), &W_(nm13 + 1), &LP_AT(VT, ll - 1, 0, ldvt), ldvt);
-                        dlasr(false, false, n, m - ll + 1, &W_(1), &W_(n), &LP_AT(U, 0, ll - 1, ldu), ldu);
+                        dlasr<P>(true, false, m - ll + 1, n, w2, w3, &LP_AT(VT, ll - 1, 0, ldvt), ldvt);
+                        dlasr<P>(false, false, n, m - ll + 1, w0, w1, &LP_AT(U, 0, ll - 1, ldu), ldu);
                     }
                 }
             }
         }
 #undef D_
 #undef E_
-#undef W_
     }
     for (int i = 0; i < n; ++i)
-        if (d[i] < 0.0) {
-            d[i] = -d[i];
-            if (WANT_V)
-                for (int j = 0; j < n; ++j) LP_AT(VT, i, j, ldvt) *= -1.0;
+        if (d.get(i) < 0.0) {
+            d.set(i, -d.get(i));
+            if (WANT_V) {
+                LP_PAR(P, j, n) LP_AT(VT, i, j, ldvt) *= -1.0;
+                P::sync();
+            }
         }
     // dbdsqr: descending selection sort (.LE.: the last of a tie moves)
     for (int i = 1; i <= n - 1; ++i) {
         int isub = 1;
-        double smin = d[0];
+        double smin = d.get(0);
         for (int j = 2; j <= n + 1 - i; ++j)
-            if (d[j - 1] <= smin) { isub = j; smin = d[j - 1]; }
+            if (d.get(j - 1) <= smin) { isub = j; smin = d.get(j - 1); }
         if (isub != n + 1 - i) {
-            d[isub - 1] = d[n - i];
-            d[n - i] = smin;
+            d.set(isub - 1, d.get(n - i));
+            d.set(n - i, smin);
             if (WANT_V) {
-                dswap(n, &LP_AT(VT, isub - 1, 0, ldvt), ldvt, &LP_AT(VT, n - i, 0, ldvt), ldvt);
-                dswap(n, &LP_AT(U, 0, isub - 1, ldu), 1, &LP_AT(U, 0, n - i, ldu), 1);
+                dswap<P>(n, &LP_AT(VT, isub - 1, 0, ldvt), ldvt, &LP_AT(VT, n - i, 0, ldvt), ldvt);
+                dswap<P>(n, &LP_AT(U, 0, isub - 1, ldu), 1, &LP_AT(U, 0, n - i, ldu), 1);
             }
         }
     }
@@ -777,43 +877,48 @@ TMF_LPN int dbdsqr(int n, double *d, double *e, double *VT, int ldvt, double *U,
 
 // dbdsdc('U', 'I') for n <= 25: U = VT = I, dlasdq -> dbdsqr, dlasdq's ascending
 // selection sort (.LT.), dbdsdc's descending selection sort (.GT.)
-template <bool WANT_V>
-TMF_LPN int dbdsdc(int n, double *d, double *e, double *U, int ldu, double *VT, int ldvt, double *work)
+template <bool WANT_V, class P>
+TMF_LPN int dbdsdc(int n, LVec<P> &d, LVec<P> &e, double *U, int ldu, double *VT, int ldvt)
 {
-    if (WANT_V)
-        for (int j = 0; j < n; ++j)
-            for (int i = 0; i < n; ++i) { LP_AT(U, i, j, ldu) = (i == j) ? 1.0 : 0.0; LP_AT(VT, i, j, ldvt) = (i == j) ? 1.0 : 0.0; }
+    if (WANT_V) {
+        LP_PAR(P, k, n * n) {
+            const int j = k / n, i = k - j * n;
+            LP_AT(U, i, j, ldu) = (i == j) ? 1.0 : 0.0;
+            LP_AT(VT, i, j, ldvt) = (i == j) ? 1.0 : 0.0;
+        }
+        P::sync();
+    }
     if (n == 1) {
-        if (WANT_V) { LP_AT(U, 0, 0, ldu) = fsign(1.0, d[0]); LP_AT(VT, 0, 0, ldvt) = 1.0; }
-        d[0] = __builtin_fabs(d[0]);
+        if (WANT_V) { LP_AT(U, 0, 0, ldu) = fsign(1.0, d.get(0)); LP_AT(VT, 0, 0, ldvt) = 1.0; }
+        d.set(0, __builtin_fabs(d.get(0)));
         return 0;
     }
-    const int info = dbdsqr<WANT_V>(n, d, e, VT, ldvt, U, ldu, work);
+    const int info = dbdsqr<WANT_V, P>(n, d, e, VT, ldvt, U, ldu);
     for (int i = 0; i < n; ++i) {
         int isub = i;
-        double smin = d[i];
+        double smin = d.get(i);
         for (int j = i + 1; j < n; ++j)
-            if (d[j] < smin) { isub = j; smin = d[j]; }
+            if (d.get(j) < smin) { isub = j; smin = d.get(j); }
         if (isub != i) {
-            d[isub] = d[i];
-            d[i] = smin;
+            d.set(isub, d.get(i));
+            d.set(i, smin);
             if (WANT_V) {
-                dswap(n, &LP_AT(VT, isub, 0, ldvt), ldvt, &LP_AT(VT, i, 0, ldvt), ldvt);
-                dswap(n, &LP_AT(U, 0, isub, ldu), 1, &LP_AT(U, 0, i, ldu), 1);
+                dswap<P>(n, &LP_AT(VT, isub, 0, ldvt), ldvt, &LP_AT(VT, i, 0, ldvt), ldvt);
+                dswap<P>(n, &LP_AT(U, 0, isub, ldu), 1, &LP_AT(U, 0, i, ldu), 1);
             }
         }
     }
     for (int i = 0; i < n - 1; ++i) {
         int kk = i;
-        double p = d[i];
+        double p = d.get(i);
         for (int j = i + 1; j < n; ++j)
-            if (d[j] > p) { kk = j; p = d[j]; }
+            if (d.get(j) > p) { kk = j; p = d.get(j); }
         if (kk != i) {
-            d[kk] = d[i];
-            d[i] = p;
+            d.set(kk, d.get(i));
+            d.set(i, p);
             if (WANT_V) {
-                dswap(n, &LP_AT(U, 0, i, ldu), 1, &LP_AT(U, 0, kk, ldu), 1);
-                dswap(n, &LP_AT(VT, i, 0, ldvt), ldvt, &LP_AT(VT, kk, 0, ldvt), ldvt);
+                dswap<P>(n, &LP_AT(U, 0, i, ldu), 1, &LP_AT(U, 0, kk, ldu), 1);
+                dswap<P>(n, &LP_AT(VT, i, 0, ldvt), ldvt, &LP_AT(VT, kk, 0, ldvt), ldvt);
             }
         }
     }
@@ -821,17 +926,19 @@ TMF_LPN int dbdsdc(int n, double *d, double *e, double *U, int ldu, double *VT, 
 }
 
 // dormbr('Q','L','N') -> dorm2r: H(k) ... H(1) applied backwards to U
+template <class P>
 TMF_LPN void apply_q(int n, double *A, const double *tauq, double *U, double *work)
 {
     for (int i = n - 1; i >= 0; --i) {
         const double aii = LP_AT(A, i, i, n);
         LP_AT(A, i, i, n) = 1.0;
-        dlarf(1, n - i, n, &LP_AT(A, i, i, n), 1, tauq[i], &LP_AT(U, i, 0, n), n, work);
+        dlarf<P>(1, n - i, n, &LP_AT(A, i, i, n), 1, tauq[i], &LP_AT(U, i, 0, n), n, work);
         LP_AT(A, i, i, n) = aii;
     }
 }
 
 // dormbr('P','R','T'), nq = k = n -> dorml2('R','N', n, n-1, n-1, A(1,2), taup, VT(1,2))
+template <class P>
 TMF_LPN void apply_pt(int n, double *A, const double *taup, double *VT, double *work)
 {
     if (n <= 1) return;
@@ -840,7 +947,7 @@ TMF_LPN void apply_pt(int n, double *A, const double *taup, double *VT, double *
     for (int i = n - 2; i >= 0; --i) {
         const double aii = A2[i + i * n];
         A2[i + i * n] = 1.0;
-        dlarf(0, n, n - 1 - i, &A2[i + i * n], n, taup[i], C2 + i * n, n, work);
+        dlarf<P>(0, n, n - 1 - i, &A2[i + i * n], n, taup[i], C2 + i * n, n, work);
         A2[i + i * n] = aii;
     }
 }
@@ -851,36 +958,45 @@ TMF_LPI constexpr int ws_doubles(int n) { return 3 * n * n + 9 * n; }
 
 // np.linalg.svd of one float32 n x n block (row-major D): f32 U (row-major u[r][k]),
 // S, Vt (row-major vt[k][j]) exactly as numpy returns them, in the caller's workspace
-// ws (ws_doubles(n)).  Returns dbdsqr's info.
-template <bool WANT_V>
+// ws (ws_doubles(n)).  Returns dbdsqr's info (0, or 1: not converged -- np.linalg.svd
+// raises LinAlgError there).  Under WavePar every lane of the wave calls it for the same
+// block, with ws, D and the outputs in LDS or global memory visible to the whole wave.
+template <bool WANT_V, class P = SerialPar>
 TMF_LPN int svd_f32_ws(const float *D, int n, float *Uo, float *So, float *Vto, double *ws)
 {
     double *A = ws, *U = A + n * n, *VT = U + n * n, *d = VT + n * n, *e = d + n, *tauq = e + n, *taup = tauq + n,
            *work = taup + n;
-    for (int i = 0; i < n; ++i)
-        for (int j = 0; j < n; ++j) A[i + j * n] = (double)D[i * n + j];
-    // dgesdd scales only when max|a| is outside [sqrt(safmin)/prec, its inverse]: never for f32 data
-    dgebd2(n, A, n, d, e, tauq, taup, work);
-    const int info = dbdsdc<WANT_V>(n, d, e, U, n, VT, n, work);
-    if (WANT_V) {
-        apply_q(n, A, tauq, U, work);
-        apply_pt(n, A, taup, VT, work);
-        for (int i = 0; i < n; ++i)
-            for (int k = 0; k < n; ++k) {
-                Uo[i * n + k] = (float)U[i + k * n];
-                Vto[i * n + k] = (float)VT[i + k * n];
-            }
+    LP_PAR(P, k, n * n) {
+        const int j = k / n, i = k - j * n;
+        A[i + j * n] = (double)D[i * n + j];
     }
-    for (int k = 0; k < n; ++k) So[k] = (float)d[k];
+    P::sync();
+    // dgesdd scales only when max|a| is outside [sqrt(safmin)/prec, its inverse]: never for f32 data
+    dgebd2<P>(n, A, n, d, e, tauq, taup, work);
+    LVec<P> dv, ev;
+    dv.load(d, n);
+    ev.load(e, n - 1);
+    const int info = dbdsdc<WANT_V, P>(n, dv, ev, U, n, VT, n);
+    if (WANT_V) {
+        apply_q<P>(n, A, tauq, U, work);
+        apply_pt<P>(n, A, taup, VT, work);
+        LP_PAR(P, q, n * n) {
+            const int i = q / n, k = q - i * n;
+            Uo[i * n + k] = (float)U[i + k * n];
+            Vto[i * n + k] = (float)VT[i + k * n];
+        }
+    }
+    dv.store_f32(So, n);
+    P::sync();
     return info;
 }
 
-// the same with a private workspace (stage entry point, host builds)
-template <bool WANT_V>
+// the same with a private workspace (host builds)
+template <bool WANT_V, class P = SerialPar>
 TMF_LPN int svd_f32(const float *D, int n, float *Uo, float *So, float *Vto)
 {
     double ws[ws_doubles(kMaxN)];
-    return svd_f32_ws<WANT_V>(D, n, Uo, So, Vto, ws);
+    return svd_f32_ws<WANT_V, P>(D, n, Uo, So, Vto, ws);
 }
 
 }  // namespace lp

@@ -1,0 +1,71 @@
+#!/usr/bin/env python3
+"""Latency of the app's per-image calls through the drop-in (host PIL images in, PIL out):
+embed_watermark(img, qr_png_bytes, preserve_ratio=True) as the embed page calls it
+(internal_pages/embed_watermark_page.py:529-531) and extract_watermark(wm, orig)
+(extract_watermark_page.py:293-296), on a camera-like 1080p image and a QR watermark.
+Also the same embed as a device-resident batch of one frame (batch.embed_batch), which
+excludes PIL and PCIe.  Prints one JSON line (median ms over --reps calls after one warm-up)."""
+import argparse
+import io
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+from PIL import Image  # noqa: E402
+
+from thatsmyface_amd import batch  # noqa: E402
+from thatsmyface_amd import watermarking as W  # noqa: E402
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--reps", type=int, default=20)
+    p.add_argument("--height", type=int, default=1080)
+    p.add_argument("--width", type=int, default=1920)
+    p.add_argument("--block", type=int, default=8)
+    a = p.parse_args()
+    from golden.gen_golden import wmark
+    from lapack_path import photo_cover
+
+    cover = Image.fromarray(photo_cover(a.height, a.width, 5))
+    qr = Image.fromarray(wmark("qr", 300, 300, 3))
+    buf = io.BytesIO()
+    qr.save(buf, format="PNG")
+    png = buf.getvalue()
+    cs = {"block_size": a.block, "alpha": 0.1}
+
+    def timed(fn):
+        fn()
+        t = []
+        for _ in range(a.reps):
+            t0 = time.perf_counter()
+            fn()
+            t.append((time.perf_counter() - t0) * 1e3)
+        return round(statistics.median(t), 3)
+
+    out = {}
+    wm_img = W.embed_watermark(cover, png, True, cs)
+    out["embed_watermark_ms"] = timed(lambda: W.embed_watermark(cover, png, True, cs))
+    out["extract_watermark_ms"] = timed(lambda: W.extract_watermark(wm_img, cover, cs))
+    dev = torch.device("cuda", 0)
+    fr = torch.from_numpy(np.asarray(cover)[None].copy()).to(dev)
+    tile = batch.synth_tile(a.height // a.block, a.width // a.block, device=dev)
+    res = torch.empty_like(fr)
+
+    def dev_embed():
+        batch.embed_batch(fr, tile, a.block, 0.1, out=res)
+        torch.cuda.synchronize()
+    out["device_embed_1frame_ms"] = timed(dev_embed)
+    print(json.dumps({"image": f"{a.width}x{a.height} camera-like", "block": a.block, "reps": a.reps, **out}))
+
+
+if __name__ == "__main__":
+    main()
