@@ -236,6 +236,18 @@ def _profile_json(name):
         return None
 
 
+def kernel_code_ids():
+    """kernel -> code id of the loaded build (libtmfwm.kernels.json next to the library)."""
+    from thatsmyface_amd import _lib
+
+    path = os.path.splitext(_lib.LIB_PATH)[0] + ".kernels.json"
+    try:
+        with open(path) as f:
+            return json.load(f).get("kernels", {})
+    except (OSError, ValueError):
+        return {}
+
+
 def lib_build_id():
     """sha256 prefix of the loaded libtmfwm.so: profiles/*.json record the build they measured."""
     import hashlib
@@ -427,31 +439,38 @@ def run(args, kernels=None, device=None):
     copy_gbs = measured_copy_peak(torch, dev) if rank == 0 and on_gpu else None
     build = lib_build_id() if on_gpu else None
 
-    # HBM bytes of the embed launch: counted FETCH / WRITE bytes per frame of this build and
-    # shape (profiles/valu.json, tools/pmc_embed.sh) x frames; else the older traffic.json
-    traffic = None
+    # Counter-derived figures (tools/pmc_embed.sh -> tools/valu.py -> profiles/valu.json) are
+    # used only for the device code they measured: each entry carries the code id of its
+    # kernel's TU (tools/kernel_ids.py -> libtmfwm.kernels.json, written when the library is
+    # linked), so a rebuild that leaves the kernel's code unchanged keeps its profile.
+    ids = kernel_code_ids() if on_gpu else {}
     vj = _profile_json("valu.json")
-    ek = (vj or {}).get("kernels", {}).get(f"embed_kernel<{b}>", {})
-    if vj and vj.get("build_id") == build and (ek.get("height"), ek.get("width")) == (H, W) and ek.get("hbm_bytes_per_frame"):
-        traffic = int(ek["hbm_bytes_per_frame"] * F)
-    else:
-        tj = _profile_json("traffic.json")
-        if tj and (tj.get("build_id") in (None, build)):
-            traffic = tj.get("embed_kernel_hbm_bytes_per_launch", {}).get(f"{F}x{H}x{W}_b{b}")
 
-    # VALU-issue roofline (tools/valu.py -> profiles/valu.json, counters of THIS build): the
-    # spec-rate issue cycles per frame over this run's cycles per frame at the clock the
-    # counter pass measured (GRBM_GUI_ACTIVE), i.e. the fraction of peak VALU issue
+    def profiled(name):
+        k = (vj or {}).get("kernels", {}).get(name)
+        if k and k.get("code_id") and k.get("code_id") == ids.get(name) and (k.get("height"), k.get("width")) == (H, W):
+            return k
+        return None
+
+    # HBM bytes of the embed launch: counted FETCH / WRITE bytes per frame x frames
+    traffic = None
+    ek = profiled(f"embed_kernel<{b}>")
+    if ek and ek.get("hbm_bytes_per_frame"):
+        traffic = int(ek["hbm_bytes_per_frame"] * F)
+
+    # VALU-issue roofline: the spec-rate issue cycles per frame over this run's cycles per
+    # frame at the clock the counter pass measured (GRBM_GUI_ACTIVE), i.e. the fraction of
+    # peak VALU issue
     valu = {}
-    if vj and vj.get("build_id") == build:
-        for name, ms in ((f"embed_kernel<{b}>", embed_ms), (f"extract_kernel<{b}>", extract_ms)):
-            k = vj.get("kernels", {}).get(name)
-            if k and (k.get("height"), k.get("width")) == (H, W) and k.get("clock_MHz"):
-                got = ms * 1e3 / F
-                frac = k["issue_bound_cycles_per_frame"] / (got * k["clock_MHz"])
-                valu[name] = {"valu_instr_per_wave": k["valu_instr_per_wave"], "f64_per_wave": k["f64_arith_per_wave"],
-                              "bound_us_per_frame_at_clock": k["valu_issue_bound_us_per_frame"],
-                              "clock_MHz": k["clock_MHz"], "us_per_frame": round(got, 2), "issue_fraction": round(frac, 3)}
+    for name, ms in ((f"embed_kernel<{b}>", embed_ms), (f"extract_kernel<{b}>", extract_ms)):
+        k = profiled(name)
+        if k and k.get("clock_MHz"):
+            got = ms * 1e3 / F
+            frac = k["issue_bound_cycles_per_frame"] / (got * k["clock_MHz"])
+            valu[name] = {"valu_instr_per_wave": k["valu_instr_per_wave"], "f64_per_wave": k["f64_arith_per_wave"],
+                          "bound_us_per_frame_at_clock": k["valu_issue_bound_us_per_frame"],
+                          "clock_MHz": k["clock_MHz"], "us_per_frame": round(got, 2), "issue_fraction": round(frac, 3),
+                          "code_id": k["code_id"]}
 
     if rank == 0:
         is4k = (H, W) == (2160, 3840)
@@ -505,6 +524,7 @@ def run(args, kernels=None, device=None):
             "cpu_baseline": cpu,
             "cpu_baseline_reference_model": structured,
             "lib_build": build,
+            "kernel_code_ids": {k: ids.get(k) for k in (f"embed_kernel<{b}>", f"extract_kernel<{b}>")} if on_gpu else None,
         }
         if world > 1 and args.backend == "gloo":
             line["rehearsal"] = f"gloo: {world} ranks on {n_phys} device(s); not a multi-GPU measurement"

@@ -163,39 +163,27 @@ TMF_DEVI void load_block_rows(const uint8_t *frame_base, int W, const StripPos &
     }
 }
 
-// Per-channel unit values from a 256-entry LDS table (luma_t / chroma_t) instead of
-// converting every byte: same values, same bits, fewer VALU operations per pixel.
-#ifndef TMF_UNIT_LUT
-#define TMF_UNIT_LUT 0
-#endif
-
 template <int B>
-TMF_DEVI void luma_rows(const uint32_t (&words)[Geo<B>::R][Geo<B>::NW], float (&y)[Geo<B>::R][B], const double *ut)
+TMF_DEVI void luma_rows(const uint32_t (&words)[Geo<B>::R][Geo<B>::NW], float (&y)[Geo<B>::R][B])
 {
 #pragma unroll
     for (int r = 0; r < Geo<B>::R; ++r)
 #pragma unroll
         for (int c = 0; c < B; ++c) {
             const uint32_t R8 = byte_at(words[r], 3 * c), G8 = byte_at(words[r], 3 * c + 1), B8 = byte_at(words[r], 3 * c + 2);
-            y[r][c] = TMF_UNIT_LUT ? luma_t(ut, R8, G8, B8) : luma(R8, G8, B8);
+            y[r][c] = luma(R8, G8, B8);
         }
 }
 
 // ---------------------------------------------------------------------------
 // Embed: watermarking.py:163-216 fused, one launch per batch.
 // ---------------------------------------------------------------------------
-#ifndef TMF_EMBED_WAVES_BIG
-#define TMF_EMBED_WAVES_BIG 2
-#endif
 // Waves per SIMD the register allocation must allow (1 = unconstrained: the compiler
 // then fits b <= 10 and 14 into 2-3 waves, but b = 12 and 16 overflow into AGPRs and run
 // one wave per SIMD).  Forcing 2 for b = 12 / 16 costs 156 / 256 B of scratch per lane
 // and is faster: embed<12> 283 -> 201 us, embed<16> 531 -> 345 us per 4K frame.
-#ifndef TMF_EMBED8_WAVES
-#define TMF_EMBED8_WAVES 1
-#endif
 template <int B>
-constexpr int kEmbedWaves = (B == 12 || B == 16) ? TMF_EMBED_WAVES_BIG : B == 8 ? TMF_EMBED8_WAVES : 1;
+constexpr int kEmbedWaves = (B == 12 || B == 16) ? 2 : 1;
 
 template <int B>
 __global__ __launch_bounds__(64, kEmbedWaves<B>) void embed_kernel(EmbedArgs a)
@@ -203,9 +191,7 @@ __global__ __launch_bounds__(64, kEmbedWaves<B>) void embed_kernel(EmbedArgs a)
     constexpr int L = Geo<B>::L, R = Geo<B>::R, BPW = Geo<B>::BPW, LD = B + 1, NW = Geo<B>::NW;
     __shared__ __attribute__((aligned(16))) float lds[BPW * B * LD];  // also the column norms during the SVD
     __shared__ uint32_t pix[R * NW][64];  // this lane's source bytes, parked during the SVD
-    __shared__ double ut[TMF_UNIT_LUT ? 256 : 1];  // unit values of the 256 byte values
     const int lane = threadIdx.x & 63, g = lane / L, q = lane % L;
-    if constexpr (TMF_UNIT_LUT) fill_unit_table(ut, lane);  // read after dct2d's first barrier
     float *tile = lds + g * B * LD;
     const StripPos pos = strip_pos<B>(a.strips_per_row, a.nbw);
     const uint8_t *src = a.src + pos.frame * a.frame_stride;
@@ -216,8 +202,7 @@ __global__ __launch_bounds__(64, kEmbedWaves<B>) void embed_kernel(EmbedArgs a)
     {
         uint32_t words[R][NW];
         load_block_rows<B>(src, a.W, pos, q, a.aligned, words);
-        if constexpr (TMF_UNIT_LUT) __syncthreads();
-        luma_rows<B>(words, x, ut);
+        luma_rows<B>(words, x);
 #pragma unroll
         for (int r = 0; r < R; ++r)
 #pragma unroll
@@ -354,8 +339,7 @@ __global__ __launch_bounds__(64, kEmbedWaves<B>) void embed_kernel(EmbedArgs a)
             for (int c = 0; c < B; ++c) {
                 float cbs, crs;
                 const uint32_t R0 = byte_at(words[r], 3 * c), G0 = byte_at(words[r], 3 * c + 1), B0 = byte_at(words[r], 3 * c + 2);
-                if constexpr (TMF_UNIT_LUT) chroma_t(ut, R0, G0, B0, cbs, crs);
-                else chroma(R0, G0, B0, cbs, crs);
+                chroma(R0, G0, B0, cbs, crs);
                 uint32_t R8, G8, B8;
                 colour_inv(x[r][c], cbs, crs, R8, G8, B8);
                 const int k0 = 3 * c;

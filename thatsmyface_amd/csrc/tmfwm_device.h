@@ -48,27 +48,6 @@ TMF_DEVI void chroma(uint32_t R, uint32_t G, uint32_t B, float &cbs, float &crs)
     crs = (float)__builtin_fma(-0.081, b, __builtin_fma(0.5, r, -0.419 * g)) + 0.5f;
 }
 
-// The same two functions on pre-converted channels: ut[v] == (double)unit_from_u8(v), a
-// 256-entry table in LDS (one ds_read_b64 per channel instead of the byte conversion,
-// the correctly rounded divide and the widening).  Same operations, same bits.
-TMF_DEVI float luma_t(const double *ut, uint32_t R, uint32_t G, uint32_t B)
-{
-    const double r = ut[R], g = ut[G], b = ut[B];
-    return (float)__builtin_fma(0.114, b, __builtin_fma(0.299, r, 0.587 * g));
-}
-TMF_DEVI void chroma_t(const double *ut, uint32_t R, uint32_t G, uint32_t B, float &cbs, float &crs)
-{
-    const double r = ut[R], g = ut[G], b = ut[B];
-    cbs = (float)__builtin_fma(0.5, b, __builtin_fma(-0.169, r, -0.331 * g)) + 0.5f;
-    crs = (float)__builtin_fma(-0.081, b, __builtin_fma(0.5, r, -0.419 * g)) + 0.5f;
-}
-// fill a wave's table: 4 entries per lane
-TMF_DEVI void fill_unit_table(double *ut, int lane)
-{
-#pragma unroll
-    for (int k = 0; k < 4; ++k) ut[lane + 64 * k] = (double)unit_from_u8((uint32_t)(lane + 64 * k));
-}
-
 // np.clip(.,0,1) in f32, * 255 in f32, astype(uint8) = truncation (watermarking.py:70-73).
 // The clip is one v_med3_f32; it differs from np.clip only in the sign of a zero
 // result (and on NaN, which no finite pixel produces), and -0 * 255 truncates to 0 too.
@@ -628,30 +607,19 @@ TMF_DEVI void dct3(float (&c)[N])
 // oracle's balanced pairwise tree); round-robin pair schedule; the rotation
 // tests and the IEEE-only rotation formula of oracle rotation()/rotationf().
 // ---------------------------------------------------------------------------
-// TMF_F32_SWEEPS / TMF_F64_SWEEPS override the sweep caps for timing experiments
-// only (tools/time_embed.py); the contract values are the defaults.
-#ifndef TMF_F32_SWEEPS
-#define TMF_F32_SWEEPS 4
-#endif
-#ifndef TMF_F64_SWEEPS
-#define TMF_F64_SWEEPS 32
-#endif
-#ifndef TMF_F64_BRANCHY
-#define TMF_F64_BRANCHY 1
-#endif
 // kBranchy: skip a pair's rotation / update when no block of the wave rotates it
 // (pays off in the converging f64 sweeps); branch-free otherwise (the f32 sweeps
 // rotate nearly every pair somewhere in the wave, and a join costs register moves).
 template <typename T> struct JacP;
 template <> struct JacP<double> {
-    static constexpr bool kBranchy = TMF_F64_BRANCHY;
-    static constexpr int kMaxSweeps = TMF_F64_SWEEPS;
+    static constexpr bool kBranchy = true;
+    static constexpr int kMaxSweeps = 32;
     static constexpr double kTol2 = 7.888609052210118e-31;  // 2^-100
     static constexpr double kC2 = 9.860761315262648e-32;    // 2^-103
 };
 template <> struct JacP<float> {
     static constexpr bool kBranchy = false;
-    static constexpr int kMaxSweeps = TMF_F32_SWEEPS;
+    static constexpr int kMaxSweeps = 4;
     static constexpr float kTol2 = 9.094947017729282e-13f;  // 2^-40
     static constexpr float kC2 = 2.842170943040401e-14f;    // 2^-45
     static constexpr float kC2A = 3.552713678800501e-15f;   // 2^-48
@@ -803,16 +771,13 @@ TMF_DEVI double rsqrt_n(double x)
     }
     return y;
 }
-#ifndef TMF_RSQF_ITERS
-#define TMF_RSQF_ITERS 3
-#endif
 TMF_DEVI float rsqrt_n(float x)
 {
     const unsigned i = 0x5f375a86u - (__builtin_bit_cast(unsigned, x) >> 1);
     float y = __builtin_bit_cast(float, i);
     const float hx = 0.5f * x;
 #pragma unroll
-    for (int k = 0; k < TMF_RSQF_ITERS; ++k) {
+    for (int k = 0; k < 3; ++k) {
         const float t = y * y;
         const float u = __builtin_fmaf(-hx, t, 1.5f);
         y = y * u;
@@ -886,46 +851,22 @@ constexpr int kRows = (B + L - 1) / L;
 // when it rotates, writes them back updated.  Same operations on the same values as the
 // register form, so the same bits; 32 fewer live VGPRs (the norms) in the f64 phase,
 // ~40 fewer VALU operations and 16 fewer broadcasts (t*gamma) per round.
-#ifndef TMF_LDS_NORMS
-#define TMF_LDS_NORMS 1
-#endif
-#ifndef TMF_LN_MIN_L  // smallest block group that keeps its norms in LDS (timing experiments)
-#define TMF_LN_MIN_L 8
-#endif
-template <int L>
-constexpr bool kLdsNorms = TMF_LDS_NORMS && L >= 2 && L >= TMF_LN_MIN_L;
-#ifndef TMF_LN_TYPES  // which phases keep their norms in LDS (timing experiments: tools/build_variant.sh)
-#define TMF_LN_TYPES(T) (std::is_same_v<T, double>)
-#endif
+template <int L, typename T>
+constexpr bool kLdsNorms = L == 8 && std::is_same_v<T, double>;  // the f64 phase (the f32 one: one wave / SIMD at b = 14)
 
 // Rotation parameters through LDS (8-lane blocks): the owner of each pair writes its
 // (c, s) next to the norms and every lane of the block reads the pairs it applies
 // (ds_write2 + one ds_read2 per pair), instead of two ds_swizzle per 32-bit half of each
 // broadcast value.  Pure data movement: the same bits.
-#ifndef TMF_LDS_BCAST
-#define TMF_LDS_BCAST 1
-#endif
-#ifndef TMF_LB_TYPES
-#define TMF_LB_TYPES(T) true
-#endif
-#ifndef TMF_LB_MIN_L  // smallest block group that broadcasts through LDS (timing experiments)
-#define TMF_LB_MIN_L 8
-#endif
 template <int L>
-constexpr bool kLdsBcast = TMF_LDS_BCAST && L >= 2 && L >= TMF_LB_MIN_L;
+constexpr bool kLdsBcast = L == 8;  // 2- and 4-lane groups: DPP moves (LDS measured within noise there)
 
 // Pair dot products through LDS (8-lane blocks, one pair per lane): only the owner of a
 // pair needs its gamma, so instead of the 3-level DPP butterfly for every pair on every
 // lane, each lane writes its partials and the owner sums its pair's 8 partials in the
 // butterfly's tree order ((p0+p1)+(p2+p3))+((p4+p5)+(p6+p7)) -- the same bits.
-#ifndef TMF_LDS_SUMS
-#define TMF_LDS_SUMS 1
-#endif
-#ifndef TMF_LS_TYPES  // which phases sum through LDS (timing experiments)
-#define TMF_LS_TYPES(T) (std::is_same_v<T, double>)
-#endif
-template <int L>
-constexpr bool kLdsSums = TMF_LDS_SUMS && L == 8;
+template <int L, typename T>
+constexpr bool kLdsSums = L == 8 && std::is_same_v<T, double>;
 
 // pair p's lower / higher column for every p < b/2 of round s, one 4-bit field per lane
 // p; a lane without a pair (p >= b/2: b = 14) gets slot 15, a dummy past the b norms
@@ -953,14 +894,14 @@ TMF_DEVI int jacobi_sweep(T (&A)[(B + L - 1) / L][B], T (&V)[(B + L - 1) / L][B]
     // NP pairs per round; lane q evaluates pairs [q*PP, q*PP + PP) that exist
     constexpr int R = kRows<B, L>, NP = B / 2, PP = (NP + L - 1) / L;
     constexpr bool kBranchy = P::kBranchy;
-    constexpr bool kLN = kLdsNorms<L> && TMF_LN_TYPES(T);
-    constexpr bool kLB = kLdsBcast<L> && TMF_LB_TYPES(T);
+    constexpr bool kLN = kLdsNorms<L, T>;
+    constexpr bool kLB = kLdsBcast<L>;
     static_assert(!kLN || NP <= 8, "LDS norms: 4-bit pair table");
     static_assert(!kLB || L * PP <= 8, "LDS broadcast: 8 parameter slots");
     // kLB: (c, s) of pair slot p at prm[2p], prm[2p+1] (after the 16 norms when those are
     // in LDS too), t*gamma at prm[16 + p] when the norms are replicated on the lanes
     T *prm = nl + (kLN ? 16 : 0);
-    constexpr bool kLS = kLdsSums<L> && TMF_LS_TYPES(T) && PP == 1;
+    constexpr bool kLS = kLdsSums<L, T> && PP == 1;
     T *part = nl + 32;  // kLS: partial of pair p from lane k at part[p * 8 + k]
     T nrm[B];
     // batches of dot products: all lane-local chains first, then all cross-lane sums,

@@ -14,41 +14,32 @@
 
 namespace tmf {
 
-#ifndef TMF_EMBED8_HERE
 extern template __global__ void embed_kernel<8>(EmbedArgs);  // tmfwm_embed8.hip
-#endif
 
 // ---------------------------------------------------------------------------
 // Extract: watermarking.py:241-289 fused; sigma_1 of both images per block.
 // ---------------------------------------------------------------------------
-#ifndef TMF_POWER_ITERS
-#define TMF_POWER_ITERS 6
-#endif
-constexpr int kPowerIters = TMF_POWER_ITERS;
-#ifndef TMF_EXTRACT8_WAVES
-#define TMF_EXTRACT8_WAVES 3
-#endif  // f32 power iterations before certification
+constexpr int kPowerIters = 6;    // f32 power iterations before certification
+constexpr int kExtract8Waves = 3;  // waves per SIMD the register allocation of extract<b <= 8> allows
 
 template <int B>
-TMF_DEVI bool sigma1_of(const uint32_t (&words)[Geo<B>::R][Geo<B>::NW], int q, float *tile, const double *ut, float &s1)
+TMF_DEVI bool sigma1_of(const uint32_t (&words)[Geo<B>::R][Geo<B>::NW], int q, float *tile, float &s1)
 {
     constexpr int L = Geo<B>::L, R = Geo<B>::R;
     float x[R][B];
-    luma_rows<B>(words, x, ut);
+    luma_rows<B>(words, x);
     dct2d_rows_layout<B, false>(x, tile, q);
     return sigma1_certified<B, L, kPowerIters>(x, s1);
 }
 
 template <int B>
-__global__ __launch_bounds__(64, (B > 8 ? 2 : TMF_EXTRACT8_WAVES)) void extract_kernel(ExtractArgs a)  // waves per SIMD
+__global__ __launch_bounds__(64, (B > 8 ? 2 : kExtract8Waves)) void extract_kernel(ExtractArgs a)  // waves per SIMD
 {
     constexpr int L = Geo<B>::L, BPW = Geo<B>::BPW, LD = B + 1;
     __shared__ float lds[BPW * B * LD];
-    __shared__ double ut[TMF_UNIT_LUT ? 256 : 1];  // unit values of the 256 byte values
     const int lane = threadIdx.x & 63, g = lane / L, q = lane % L;
     float *tile = lds + g * B * LD;
     const StripPos pos = strip_pos<B>(a.strips_per_row, a.nbw);
-    if constexpr (TMF_UNIT_LUT) fill_unit_table(ut, lane);
     // b <= 12: both images' rows are requested up front -- one exposed HBM latency per
     // wave, not two (~4 % at b = 8, and only at 3 waves/SIMD, hence the launch bound).
     float sw, so;
@@ -57,16 +48,14 @@ __global__ __launch_bounds__(64, (B > 8 ? 2 : TMF_EXTRACT8_WAVES)) void extract_
         uint32_t ww[Geo<B>::R][Geo<B>::NW], wo[Geo<B>::R][Geo<B>::NW];
         load_block_rows<B>(a.wsrc + pos.frame * a.frame_stride, a.W, pos, q, a.aligned, ww);
         load_block_rows<B>(a.osrc + pos.frame * a.frame_stride, a.W, pos, q, a.aligned, wo);
-        if constexpr (TMF_UNIT_LUT) __syncthreads();
-        ok = sigma1_of<B>(ww, q, tile, ut, sw);
-        ok = sigma1_of<B>(wo, q, tile, ut, so) && ok;
+        ok = sigma1_of<B>(ww, q, tile, sw);
+        ok = sigma1_of<B>(wo, q, tile, so) && ok;
     } else {
         uint32_t w[Geo<B>::R][Geo<B>::NW];
         load_block_rows<B>(a.wsrc + pos.frame * a.frame_stride, a.W, pos, q, a.aligned, w);
-        if constexpr (TMF_UNIT_LUT) __syncthreads();
-        ok = sigma1_of<B>(w, q, tile, ut, sw);
+        ok = sigma1_of<B>(w, q, tile, sw);
         load_block_rows<B>(a.osrc + pos.frame * a.frame_stride, a.W, pos, q, a.aligned, w);
-        ok = sigma1_of<B>(w, q, tile, ut, so) && ok;
+        ok = sigma1_of<B>(w, q, tile, so) && ok;
     }
     if (!pos.valid || q != 0) return;
     const uint32_t id = (uint32_t)(((int64_t)blockIdx.y * a.nbh + pos.bi) * a.nbw + pos.bj);

@@ -56,14 +56,17 @@ def main():
     p.add_argument("--height", type=int, default=2160)
     p.add_argument("--width", type=int, default=3840)
     p.add_argument("--build", default=None, help="sha256 prefix of the measured libtmfwm.so (bench.py lib_build)")
+    p.add_argument("--ids", default="thatsmyface_amd/libtmfwm.kernels.json",
+                   help="the measured build's kernel code ids (tools/kernel_ids.py, written by the Makefile)")
     p.add_argument("--out", default="profiles/valu.json")
     a = p.parse_args()
     block, frames = (int(v) for v in open(os.path.join(a.pmc_dir, "block")).read().split())
+    ids = json.load(open(a.ids))["kernels"] if os.path.exists(a.ids) else {}
     out = {}
     if os.path.exists(a.out):
         old = json.load(open(a.out))
-        if old.get("build_id") == a.build and "spec_issue_cycles" in old:
-            out = old
+        if "spec_issue_cycles" in old:
+            out = old  # entries are keyed by kernel and carry the code id they measured
     out.update({
         "build_id": a.build,
         "spec_issue_cycles": CYC,
@@ -102,6 +105,8 @@ def main():
             ent["issue_fraction_profiled"] = round(ent["valu_issue_bound_us_per_frame"] / ent["profiled_us_per_frame"], 3)
         if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
             ent["hbm_bytes_per_frame"] = round((2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024 / frames)
+        ent["code_id"] = ids.get(f"{k}<{block}>")
+        ent["build_id"] = a.build
         out["kernels"][f"{k}<{block}>"] = ent
     with open(a.out, "w") as f:
         json.dump(out, f, indent=1)
