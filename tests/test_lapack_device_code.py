@@ -26,8 +26,10 @@ def host():
         pytest.skip("hipcc not available")
     if not os.path.exists(OUT) or os.path.getmtime(OUT) < max(os.path.getmtime(SRC), os.path.getmtime(HDR)):
         os.makedirs(os.path.dirname(OUT), exist_ok=True)
+        tmp = f"{OUT}.{os.getpid()}.tmp"  # pytest-xdist workers may build at once: write aside, rename
         subprocess.run([HIPCC, "-O2", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-x", "hip",
-                        "--offload-arch=gfx950", "-shared", "-o", OUT, SRC], check=True)
+                        "--offload-arch=gfx950", "-shared", "-o", tmp, SRC], check=True)
+        os.replace(tmp, OUT)
     L = ctypes.CDLL(OUT)
     L.lp_host_dnrm2.restype = ctypes.c_double
     L.lp_host_dnrm2.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
