@@ -1280,84 +1280,90 @@ TMF_DEVI int svd3(const float (&D)[(B + L - 1) / L][B], double (&A)[(B + L - 1) 
 // If both ends round to the same float, that float IS f32(sigma_1) of the
 // reference; otherwise the caller falls back to the exact Jacobi.
 // ---------------------------------------------------------------------------
-template <int B, int L, int ITERS>
-TMF_DEVI bool sigma1_certified(const float (&x)[(B + L - 1) / L][B], float &s1)
+template <int B, int L, int ITERS, int NI>
+TMF_DEVI void sigma1_certified(const float (&x)[NI][(B + L - 1) / L][B], float (&s1)[NI], bool (&ok)[NI])
 {
+    // NI images side by side: the same operations per image, interleaved, so that the
+    // dependent chains of one image's power iteration overlap the other's
     constexpr int R = kRows<B, L>;
     constexpr double u = 1.1102230246251565e-16;  // 2^-53
-    float v[B];
+    float v[NI][B];
 #pragma unroll
-    for (int j = 0; j < B; ++j) v[j] = j == 0 ? 1.0f : 0.0f;
+    for (int m = 0; m < NI; ++m)
+#pragma unroll
+        for (int j = 0; j < B; ++j) v[m][j] = j == 0 ? 1.0f : 0.0f;
 #pragma unroll
     for (int it = 0; it < ITERS; ++it) {
-        float uu[R];
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-            float acc = 0.0f;
+        for (int m = 0; m < NI; ++m) {
+            float uu[R];
 #pragma unroll
-            for (int j = 0; j < B; ++j) acc = __builtin_fmaf(x[r][j], v[j], acc);
-            uu[r] = acc;
+            for (int r = 0; r < R; ++r) {
+                float acc = 0.0f;
+#pragma unroll
+                for (int j = 0; j < B; ++j) acc = __builtin_fmaf(x[m][r][j], v[m][j], acc);
+                uu[r] = acc;
+            }
+            float w[B], nn = 0.0f;
+#pragma unroll
+            for (int j = 0; j < B; ++j) {
+                float acc = 0.0f;
+#pragma unroll
+                for (int r = 0; r < R; ++r) acc = __builtin_fmaf(x[m][r][j], uu[r], acc);
+                w[j] = group_sum<L>(acc);
+                nn = __builtin_fmaf(w[j], w[j], nn);
+            }
+            const bool live = nn > 1e-30f;
+            const float inv = __builtin_amdgcn_rsqf(live ? nn : 1.0f);
+#pragma unroll
+            for (int j = 0; j < B; ++j) v[m][j] = live ? w[j] * inv : v[m][j];
         }
-        float w[B], nn = 0.0f;
+    }
+#pragma unroll
+    for (int m = 0; m < NI; ++m) {
+        double Fp = 0.0;
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int j = 0; j < B; ++j) Fp = __builtin_fma((double)x[m][r][j], (double)x[m][r][j], Fp);
+        const double F = group_sum<L>(Fp);
+        double vd[B], nv = 0.0;
 #pragma unroll
         for (int j = 0; j < B; ++j) {
-            float acc = 0.0f;
-#pragma unroll
-            for (int r = 0; r < R; ++r) acc = __builtin_fmaf(x[r][j], uu[r], acc);
-            w[j] = group_sum<L>(acc);
-            nn = __builtin_fmaf(w[j], w[j], nn);
+            vd[j] = (double)v[m][j];
+            nv = __builtin_fma(vd[j], vd[j], nv);
         }
-        const bool live = nn > 1e-30f;
-        const float inv = __builtin_amdgcn_rsqf(live ? nn : 1.0f);
+        double ud[R], ap = 0.0;
 #pragma unroll
-        for (int j = 0; j < B; ++j) v[j] = live ? w[j] * inv : v[j];
+        for (int r = 0; r < R; ++r) {
+            double acc = 0.0;
+#pragma unroll
+            for (int j = 0; j < B; ++j) acc = __builtin_fma((double)x[m][r][j], vd[j], acc);
+            ud[r] = acc;
+            ap = __builtin_fma(acc, acc, ap);
+        }
+        const double a = group_sum<L>(ap);
+        const double rho = a / nv;
+        double rn2 = 0.0;
+#pragma unroll
+        for (int j = 0; j < B; ++j) {
+            double acc = 0.0;
+#pragma unroll
+            for (int r = 0; r < R; ++r) acc = __builtin_fma((double)x[m][r][j], ud[r], acc);
+            const double rj = group_sum<L>(acc) - rho * vd[j];
+            rn2 = __builtin_fma(rj, rj, rn2);
+        }
+        const double rr0 = __builtin_sqrt(rn2 / nv) * (1.0 + 16.0 * u) + 256.0 * u * F;
+        const double rr = rr0 * rr0;
+        const double rlo = rho * (1.0 - 256.0 * u);
+        const double fhi = F * (1.0 + 256.0 * u);
+        const double gap = (rlo + rlo) - fhi;
+        const double hi = (rho + rr / (gap > 0.0 ? gap : 1.0)) * (1.0 + 256.0 * u);
+        const double slo = __builtin_sqrt(rlo) * (1.0 - 512.0 * u);
+        const double shi = __builtin_sqrt(hi) * (1.0 + 512.0 * u);
+        s1[m] = F == 0.0 ? 0.0f : (float)slo;
+        ok[m] = F == 0.0 || (gap > 0.0 && (float)shi == (float)slo && rho == rho);
     }
-    double Fp = 0.0;
-#pragma unroll
-    for (int r = 0; r < R; ++r)
-#pragma unroll
-        for (int j = 0; j < B; ++j) Fp = __builtin_fma((double)x[r][j], (double)x[r][j], Fp);
-    const double F = group_sum<L>(Fp);
-    if (F == 0.0) {
-        s1 = 0.0f;
-        return true;
-    }
-    double vd[B], nv = 0.0;
-#pragma unroll
-    for (int j = 0; j < B; ++j) {
-        vd[j] = (double)v[j];
-        nv = __builtin_fma(vd[j], vd[j], nv);
-    }
-    double ud[R], ap = 0.0;
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        double acc = 0.0;
-#pragma unroll
-        for (int j = 0; j < B; ++j) acc = __builtin_fma((double)x[r][j], vd[j], acc);
-        ud[r] = acc;
-        ap = __builtin_fma(acc, acc, ap);
-    }
-    const double a = group_sum<L>(ap);
-    const double rho = a / nv;
-    double rn2 = 0.0;
-#pragma unroll
-    for (int j = 0; j < B; ++j) {
-        double acc = 0.0;
-#pragma unroll
-        for (int r = 0; r < R; ++r) acc = __builtin_fma((double)x[r][j], ud[r], acc);
-        const double rj = group_sum<L>(acc) - rho * vd[j];
-        rn2 = __builtin_fma(rj, rj, rn2);
-    }
-    const double rr0 = __builtin_sqrt(rn2 / nv) * (1.0 + 16.0 * u) + 256.0 * u * F;
-    const double rr = rr0 * rr0;
-    const double rlo = rho * (1.0 - 256.0 * u);
-    const double fhi = F * (1.0 + 256.0 * u);
-    const double gap = (rlo + rlo) - fhi;
-    const double hi = (rho + rr / (gap > 0.0 ? gap : 1.0)) * (1.0 + 256.0 * u);
-    const double slo = __builtin_sqrt(rlo) * (1.0 - 512.0 * u);
-    const double shi = __builtin_sqrt(hi) * (1.0 + 512.0 * u);
-    s1 = (float)slo;
-    return gap > 0.0 && (float)shi == s1 && rho == rho;
 }
 
 }  // namespace tmf

@@ -19,43 +19,57 @@ extern template __global__ void embed_kernel<8>(EmbedArgs);  // tmfwm_embed8.hip
 // ---------------------------------------------------------------------------
 // Extract: watermarking.py:241-289 fused; sigma_1 of both images per block.
 // ---------------------------------------------------------------------------
-constexpr int kPowerIters = 6;    // f32 power iterations before certification
+constexpr int kPowerIters = 4;    // f32 power iterations before certification
 constexpr int kExtract8Waves = 3;  // waves per SIMD the register allocation of extract<b <= 8> allows
 
 template <int B>
-TMF_DEVI bool sigma1_of(const uint32_t (&words)[Geo<B>::R][Geo<B>::NW], int q, float *tile, float &s1)
+TMF_DEVI void dct_rows_of(const uint32_t (&words)[Geo<B>::R][Geo<B>::NW], int q, float *tile, float (&x)[Geo<B>::R][B])
 {
-    constexpr int L = Geo<B>::L, R = Geo<B>::R;
-    float x[R][B];
     luma_rows<B>(words, x);
     dct2d_rows_layout<B, false>(x, tile, q);
-    return sigma1_certified<B, L, kPowerIters>(x, s1);
 }
 
 template <int B>
 __global__ __launch_bounds__(64, (B > 8 ? 2 : kExtract8Waves)) void extract_kernel(ExtractArgs a)  // waves per SIMD
 {
-    constexpr int L = Geo<B>::L, BPW = Geo<B>::BPW, LD = B + 1;
+    constexpr int L = Geo<B>::L, R = Geo<B>::R, BPW = Geo<B>::BPW, LD = B + 1;
     __shared__ float lds[BPW * B * LD];
     const int lane = threadIdx.x & 63, g = lane / L, q = lane % L;
     float *tile = lds + g * B * LD;
     const StripPos pos = strip_pos<B>(a.strips_per_row, a.nbw);
-    // b <= 12: both images' rows are requested up front -- one exposed HBM latency per
-    // wave, not two (~4 % at b = 8, and only at 3 waves/SIMD, hence the launch bound).
     float sw, so;
     bool ok;
     if constexpr (B <= 12) {
-        uint32_t ww[Geo<B>::R][Geo<B>::NW], wo[Geo<B>::R][Geo<B>::NW];
-        load_block_rows<B>(a.wsrc + pos.frame * a.frame_stride, a.W, pos, q, a.aligned, ww);
-        load_block_rows<B>(a.osrc + pos.frame * a.frame_stride, a.W, pos, q, a.aligned, wo);
-        ok = sigma1_of<B>(ww, q, tile, sw);
-        ok = sigma1_of<B>(wo, q, tile, so) && ok;
+        // both images' rows requested up front (one exposed HBM latency per wave, not two),
+        // and both power iterations interleaved (sigma1_certified, NI = 2)
+        float x[2][R][B];
+        {
+            uint32_t ww[R][Geo<B>::NW], wo[R][Geo<B>::NW];
+            load_block_rows<B>(a.wsrc + pos.frame * a.frame_stride, a.W, pos, q, a.aligned, ww);
+            load_block_rows<B>(a.osrc + pos.frame * a.frame_stride, a.W, pos, q, a.aligned, wo);
+            dct_rows_of<B>(ww, q, tile, x[0]);
+            dct_rows_of<B>(wo, q, tile, x[1]);
+        }
+        float s[2];
+        bool k[2];
+        sigma1_certified<B, L, kPowerIters, 2>(x, s, k);
+        sw = s[0];
+        so = s[1];
+        ok = k[0] && k[1];
     } else {
-        uint32_t w[Geo<B>::R][Geo<B>::NW];
+        uint32_t w[R][Geo<B>::NW];
+        float x[1][R][B], s[1];
+        bool k[1];
         load_block_rows<B>(a.wsrc + pos.frame * a.frame_stride, a.W, pos, q, a.aligned, w);
-        ok = sigma1_of<B>(w, q, tile, sw);
+        dct_rows_of<B>(w, q, tile, x[0]);
+        sigma1_certified<B, L, kPowerIters, 1>(x, s, k);
+        sw = s[0];
+        ok = k[0];
         load_block_rows<B>(a.osrc + pos.frame * a.frame_stride, a.W, pos, q, a.aligned, w);
-        ok = sigma1_of<B>(w, q, tile, so) && ok;
+        dct_rows_of<B>(w, q, tile, x[0]);
+        sigma1_certified<B, L, kPowerIters, 1>(x, s, k);
+        so = s[0];
+        ok = ok && k[0];
     }
     if (!pos.valid || q != 0) return;
     const uint32_t id = (uint32_t)(((int64_t)blockIdx.y * a.nbh + pos.bi) * a.nbw + pos.bj);

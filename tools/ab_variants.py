@@ -34,7 +34,10 @@ for name, fn in (("embed", lambda: batch.embed_batch(fr, tile, b, 0.1, out=out))
     e1.record()
     torch.cuda.synchronize()
     res[name] = round(e0.elapsed_time(e1) * 1000 / 2 / n, 2)
-print(json.dumps({"hash": h, "us_per_frame": res}))
+se, sx = {}, {}
+batch.embed_batch(fr, tile, b, 0.1, out=out, stats=se)
+batch.extract_batch(out, fr, b, 0.1, out=ext, stats=sx)
+print(json.dumps({"hash": h, "us_per_frame": res, "lapack_blocks": {"embed": se["lapack_blocks"], "extract": sx["lapack_blocks"]}}))
 '''
 
 

@@ -5,21 +5,31 @@
 # TU (tmfwm_fallback.hip) is recompiled with them too, otherwise the ABI / tile / QR /
 # dgesdd-route objects are the main build's (make -C thatsmyface_amd/csrc first).
 # E8SCHED=<strategy> overrides the machine scheduler of the embed<8> TU (default max-ilp).
+# SRC_SED='<sed script>' compiles the kernel TUs from a copy of the sources edited by that
+# script (e.g. SRC_SED='s/kPowerIters = 6/kPowerIters = 4/'): experiments without switches
+# in the product code.
 set -euo pipefail
 NAME=$1; shift
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 C=$ROOT/thatsmyface_amd/csrc
 make -s -C "$C" >/dev/null
 T=$(mktemp -d)
+K=$C
+if [ -n "${SRC_SED:-}" ]; then
+  K=$T/src
+  mkdir -p "$K"
+  cp "$C"/*.h "$C"/*.hip "$K"/
+  sed -i "$SRC_SED" "$K"/*.h "$K"/*.hip
+fi
 F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -fno-slp-vectorize -Wall $*"
-/opt/rocm/bin/hipcc $F -c "$C/tmfwm_kernels.hip" -o "$T/k.o" &
-/opt/rocm/bin/hipcc $F -mllvm -amdgpu-sched-strategy=${E8SCHED:-max-ilp} -c "$C/tmfwm_embed8.hip" -o "$T/e8.o" &
+/opt/rocm/bin/hipcc $F -c "$K/tmfwm_kernels.hip" -o "$T/k.o" &
+/opt/rocm/bin/hipcc $F -mllvm -amdgpu-sched-strategy=${E8SCHED:-max-ilp} -c "$K/tmfwm_embed8.hip" -o "$T/e8.o" &
 FB="$C/tmfwm_fallback.o $C/tmfwm_fixup4.o $C/tmfwm_fixup6.o $C/tmfwm_fixup8.o $C/tmfwm_fixup10.o $C/tmfwm_fixup12.o $C/tmfwm_fixup14.o $C/tmfwm_fixup16.o"
 if [ "${FALLBACK:-0}" = "1" ]; then
   FB="$T/fb.o"
-  /opt/rocm/bin/hipcc $F -c "$C/tmfwm_fallback.hip" -o "$T/fb.o" &
+  /opt/rocm/bin/hipcc $F -c "$K/tmfwm_fallback.hip" -o "$T/fb.o" &
   for b in 4 6 8 10 12 14 16; do
-    /opt/rocm/bin/hipcc $F -c "$C/tmfwm_fixup$b.hip" -o "$T/fx$b.o" &
+    /opt/rocm/bin/hipcc $F -c "$K/tmfwm_fixup$b.hip" -o "$T/fx$b.o" &
     FB="$FB $T/fx$b.o"
   done
 fi
