@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define TMFWM_ABI_VERSION 4
+#define TMFWM_ABI_VERSION 5
 
 #define TMFWM_MEM_HOST 0
 #define TMFWM_MEM_DEVICE 1
@@ -127,6 +127,26 @@ int tmfwm_rgb_to_ycbcr(const uint8_t *rgb, int64_t npix, float *ycc, int32_t mem
 
 /* ycbcr_to_rgb (watermarking.py:53): npix x 3 float32 -> RGB uint8 (clip, *255, truncate). */
 int tmfwm_ycbcr_to_rgb(const float *ycc, int64_t npix, uint8_t *rgb, int32_t mem_kind, void *hip_stream);
+
+/* Element types of the typed helper entry points below. */
+#define TMFWM_DT_F16 1
+#define TMFWM_DT_F32 2
+#define TMFWM_DT_F64 3
+
+/* rgb_to_ycbcr (watermarking.py:23-50) of a non-uint8 input: rgb holds npix x 3 float32
+ * values on the 0..255 scale, i.e. the input after the reference's own cast
+ * np.array(img, dtype=np.float32) (:29), which stays with the caller; the "/ 255.0" and
+ * the rest run here.  For integral values it equals tmfwm_rgb_to_ycbcr. */
+int tmfwm_rgb_to_ycbcr_f32(const float *rgb, int64_t npix, float *ycc, int32_t mem_kind, void *hip_stream);
+
+/* ycbcr_to_rgb (watermarking.py:53-73) of an npix x 3 array of element type dtype
+ * (TMFWM_DT_F16 = IEEE binary16 / numpy float16, _F32, _F64).  The reference computes in the
+ * input's own type (:55 img.copy()): "-= 0.5", the stored dot product, clip and "* 255" are
+ * rounded to that type, so a float64 input is not the float32 result of its cast.
+ * TMFWM_DT_F32 is tmfwm_ycbcr_to_rgb.  Non-finite inputs have no defined uint8 (neither in
+ * the reference: NaN -> uint8 is undefined in C and numpy). */
+int tmfwm_ycbcr_to_rgb_typed(const void *ycc, int32_t dtype, int64_t npix, uint8_t *rgb, int32_t mem_kind,
+                             void *hip_stream);
 
 /* apply_dct_to_block / apply_idct_to_block (watermarking.py:76, :81) on n_blocks
  * contiguous row-major block x block float32 blocks, in place. */

@@ -42,6 +42,9 @@ def lib():
         sig = {
             "orc_rgb_to_ycbcr": (None, [_u8p, I64, _f32p]),
             "orc_ycbcr_to_rgb": (None, [_f32p, I64, _u8p]),
+            "orc_rgb_to_ycbcr_f32": (None, [_f32p, I64, _f32p]),
+            "orc_ycbcr_to_rgb_f64": (None, [ctypes.c_void_p, I64, _u8p]),
+            "orc_ycbcr_to_rgb_f16": (None, [ctypes.c_void_p, I64, _u8p]),
             "orc_dct2d_blocks": (None, [_f32p, I64, I32, I32]),
             "orc_dct_rows": (None, [_f32p, I64, I32, I32]),
             "orc_svd_blocks": (I32, [_f32p, I64, I32, _f32p, _f32p, _f32p, _i32p]),
@@ -87,16 +90,32 @@ def default_threads() -> int:
 
 # --- stages ---------------------------------------------------------------
 def rgb_to_ycbcr(rgb: np.ndarray) -> np.ndarray:
-    rgb = np.ascontiguousarray(rgb, dtype=np.uint8)
+    """watermarking.py:23-50.  uint8 pixels, or any other numeric array through the
+    reference's own cast np.array(img, dtype=np.float32) (:29)."""
+    rgb = np.asarray(rgb)
     out = np.empty(rgb.shape[:-1] + (3,), np.float32)
-    lib().orc_rgb_to_ycbcr(_p(rgb, _u8p), rgb.size // 3, _p(out, _f32p))
+    if rgb.dtype == np.uint8:
+        rgb = np.ascontiguousarray(rgb)
+        lib().orc_rgb_to_ycbcr(_p(rgb, _u8p), rgb.size // 3, _p(out, _f32p))
+    else:
+        rgb = np.ascontiguousarray(rgb, dtype=np.float32)
+        lib().orc_rgb_to_ycbcr_f32(_p(rgb, _f32p), rgb.size // 3, _p(out, _f32p))
     return out
 
 
 def ycbcr_to_rgb(ycc: np.ndarray) -> np.ndarray:
-    ycc = np.ascontiguousarray(ycc, dtype=np.float32)
+    """watermarking.py:53-73 in the input's own float type (float16 / 32 / 64)."""
+    ycc = np.asarray(ycc)
     out = np.empty(ycc.shape, np.uint8)
-    lib().orc_ycbcr_to_rgb(_p(ycc, _f32p), ycc.size // 3, _p(out, _u8p))
+    if ycc.dtype == np.float64 or ycc.dtype == np.float16:
+        ycc = np.ascontiguousarray(ycc)
+        fn = lib().orc_ycbcr_to_rgb_f64 if ycc.dtype == np.float64 else lib().orc_ycbcr_to_rgb_f16
+        fn(ycc.ctypes.data, ycc.size // 3, _p(out, _u8p))
+    else:
+        if ycc.dtype != np.float32:
+            raise TypeError(f"ycbcr_to_rgb takes float16/32/64 arrays, got {ycc.dtype}")
+        ycc = np.ascontiguousarray(ycc)
+        lib().orc_ycbcr_to_rgb(_p(ycc, _f32p), ycc.size // 3, _p(out, _u8p))
     return out
 
 

@@ -1164,6 +1164,83 @@ void orc_ycbcr_to_rgb(const float *ycc, int64_t npix, uint8_t *rgb)
     for (int64_t p = 0; p < npix; ++p) colour_inv(ycc[3 * p], ycc[3 * p + 1], ycc[3 * p + 2], rgb + 3 * p);
 }
 
+/* rgb_to_ycbcr of a non-uint8 input (watermarking.py:29): rgb = np.array(img, float32)
+ * (the caller's cast), then "/ 255.0" as an f32 divide and the :37-48 rows. */
+void orc_rgb_to_ycbcr_f32(const float *rgb, int64_t npix, float *ycc)
+{
+    for (int64_t p = 0; p < npix; ++p) {
+        const double r = rgb[3 * p] / 255.0f, g = rgb[3 * p + 1] / 255.0f, b = rgb[3 * p + 2] / 255.0f;
+        ycc[3 * p] = (float)fma(0.114, b, fma(0.299, r, 0.587 * g));
+        ycc[3 * p + 1] = (float)fma(0.5, b, fma(-0.169, r, -0.331 * g)) + 0.5f;
+        ycc[3 * p + 2] = (float)fma(-0.081, b, fma(0.5, r, -0.419 * g)) + 0.5f;
+    }
+}
+
+/* ycbcr_to_rgb of a float64 input: img.copy() keeps float64 (:55), so ":58 -= 0.5", the
+ * stored dot (:64-67), np.clip (:70) and "* 255" (:73) are all f64; astype(uint8) truncates. */
+static uint8_t u8_from_unit_f64(double f)
+{
+    if (f < 0.0) f = 0.0;
+    if (f > 1.0) f = 1.0;
+    return (uint8_t)(f * 255.0);
+}
+
+void orc_ycbcr_to_rgb_f64(const double *ycc, int64_t npix, uint8_t *rgb)
+{
+    for (int64_t p = 0; p < npix; ++p) {
+        const double Y = ycc[3 * p], CB = ycc[3 * p + 1] - 0.5, CR = ycc[3 * p + 2] - 0.5;
+        rgb[3 * p] = u8_from_unit_f64(fma(1.403, CR, fma(1.0, Y, 0.0 * CB)));
+        rgb[3 * p + 1] = u8_from_unit_f64(fma(-0.714, CR, fma(1.0, Y, -0.344 * CB)));
+        rgb[3 * p + 2] = u8_from_unit_f64(fma(0.0, CR, fma(1.0, Y, 1.773 * CB)));
+    }
+}
+
+/* IEEE binary16 (numpy float16) held in doubles.  half_round(x) is the binary16 value
+ * nearest x (ties to even, gradual underflow, overflow to inf) -- numpy's
+ * npy_double_to_half, and the result of every half operation below, since numpy
+ * evaluates a half '+', '-', '*' in float32 and rounds once more to half, which for
+ * these operations equals the correctly rounded half result (24 >= 2 * 11 + 2 bits). */
+static double half_round(double x)
+{
+    if (x == 0.0 || !isfinite(x)) return x;
+    int e;
+    frexp(x, &e); /* |x| in [2^(e-1), 2^e) */
+    const int q = e - 1 < -14 ? -24 : e - 11; /* ulp exponent: 10 fraction bits; subnormals 2^-24 */
+    const double r = ldexp(nearbyint(ldexp(x, -q)), q);
+    return fabs(r) >= 65520.0 ? copysign(INFINITY, x) : r;
+}
+
+static double half_bits_to_double(uint16_t h)
+{
+    const int s = h >> 15, e = (h >> 10) & 0x1f, m = h & 0x3ff;
+    double v;
+    if (e == 0) v = ldexp((double)m, -24);
+    else if (e == 31) v = m ? NAN : INFINITY;
+    else v = ldexp((double)(m | 0x400), e - 25);
+    return s ? -v : v;
+}
+
+static uint8_t u8_from_unit_f16(double f) /* f is a half value */
+{
+    if (f < 0.0) f = 0.0;
+    if (f > 1.0) f = 1.0;
+    return (uint8_t)half_round(f * 255.0); /* the product is exact in f64, then one half rounding */
+}
+
+/* ycbcr_to_rgb of a float16 input (ycc = the raw binary16 bits): every step of the f64
+ * path above rounded back to half where numpy stores a half (:58, :64 zeros_like, :73). */
+void orc_ycbcr_to_rgb_f16(const uint16_t *ycc, int64_t npix, uint8_t *rgb)
+{
+    for (int64_t p = 0; p < npix; ++p) {
+        const double Y = half_bits_to_double(ycc[3 * p]);
+        const double CB = half_round(half_bits_to_double(ycc[3 * p + 1]) - 0.5);
+        const double CR = half_round(half_bits_to_double(ycc[3 * p + 2]) - 0.5);
+        rgb[3 * p] = u8_from_unit_f16(half_round(fma(1.403, CR, fma(1.0, Y, 0.0 * CB))));
+        rgb[3 * p + 1] = u8_from_unit_f16(half_round(fma(-0.714, CR, fma(1.0, Y, -0.344 * CB))));
+        rgb[3 * p + 2] = u8_from_unit_f16(half_round(fma(0.0, CR, fma(1.0, Y, 1.773 * CB))));
+    }
+}
+
 /* nb blocks of b x b, row-major each, in place */
 void orc_dct2d_blocks(float *blocks, int64_t nb, int b, int inverse)
 {

@@ -19,6 +19,7 @@ Outputs (tests/golden/):
 Run:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py            (cases.npz, stages.npz, meta.json)
       PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py --blocks   (cases_blocks.npz, meta_blocks.json)
       PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py --alpha    (cases_alpha.npz, meta_alpha.json)
+      PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py --helpers  (helpers.npz, meta_helpers.json)
 """
 from __future__ import annotations
 
@@ -311,8 +312,63 @@ def main() -> None:
     print("wrote", os.listdir(HERE))
 
 
+def helper_inputs() -> dict[str, np.ndarray]:
+    """Non-uint8 inputs of the module-level colour helpers (watermarking.py:23, :53)."""
+    rng = np.random.default_rng(2026)
+    special = np.array([0.0, 255.0, 254.5, 0.5, -0.0, 1e-3, 1e6, 127.5, 256.0, -1.0, 3.0, 254.999],
+                       np.float64).reshape(2, 2, 3)
+    ycc = np.stack([rng.uniform(-0.3, 1.3, (24, 24)), rng.uniform(-0.3, 1.3, (24, 24)), rng.uniform(-0.3, 1.3, (24, 24))], -1)
+    k = np.arange(256, dtype=np.float64)
+    y = np.concatenate([(k - 1e-9) / 255, (k + 1e-9) / 255, np.nextafter(k / 255, -1), k / 255])
+    edge = np.stack([y, np.full_like(y, 0.5), np.full_like(y, 0.5)], -1).reshape(32, 32, 3)
+    return {
+        "fwd_f32": rng.uniform(-30, 290, (24, 24, 3)).astype(np.float32),
+        "fwd_f64": rng.uniform(-30, 290, (24, 24, 3)),
+        "fwd_special_f64": special,
+        "fwd_i32": rng.integers(-100, 400, (24, 24, 3), dtype=np.int32),
+        "fwd_u16": rng.integers(0, 65536, (16, 16, 3), dtype=np.uint16),
+        "fwd_rgba_f64": rng.uniform(0, 255, (8, 8, 4)),
+        "inv_f64": ycc,
+        "inv_f32": ycc.astype(np.float32),
+        "inv_f16": ycc.astype(np.float16),
+        # truncation edges: Y just below / above k / 255, neutral chroma
+        "inv_edge_f64": edge,
+        "inv_edge_f16": edge.astype(np.float16),
+        "noise_u8": rng.integers(0, 256, (24, 24, 3), dtype=np.uint8),
+    }
+
+
+def main_helpers() -> None:
+    """helpers.npz + meta_helpers.json: rgb_to_ycbcr on non-uint8 arrays and
+    ycbcr_to_rgb on float16 / float32 / float64 arrays, outputs by the reference."""
+    W = _import_reference()
+    inp = helper_inputs()
+    out: dict[str, np.ndarray] = {}
+    for k, v in inp.items():
+        out["in_" + k] = v
+        if k.startswith("fwd_"):
+            out["out_" + k] = W.rgb_to_ycbcr(v)
+        elif k.startswith("inv_"):
+            out["out_" + k] = W.ycbcr_to_rgb(v)
+    ycc = W.rgb_to_ycbcr(inp["noise_u8"])
+    for dt in ("f16", "f64"):
+        a = ycc.astype(np.float16 if dt == "f16" else np.float64)
+        out[f"in_inv_noise_{dt}"] = a
+        out[f"out_inv_noise_{dt}"] = W.ycbcr_to_rgb(a)
+    del out["in_noise_u8"]
+    np.savez_compressed(os.path.join(HERE, "helpers.npz"), **out)
+    meta = {"generator": "tests/golden/gen_golden.py --helpers",
+            "reference": "/root/reference/modules/watermarking.py (rgb_to_ycbcr :23, ycbcr_to_rgb :53)",
+            "numpy": np.__version__, "sha": {k: sha(v) for k, v in sorted(out.items())}}
+    with open(os.path.join(HERE, "meta_helpers.json"), "w") as f:
+        json.dump(meta, f, indent=1, sort_keys=True)
+    print("wrote helpers.npz:", sorted(out))
+
+
 if __name__ == "__main__":
-    if "--blocks" in sys.argv[1:]:
+    if "--helpers" in sys.argv[1:]:
+        main_helpers()
+    elif "--blocks" in sys.argv[1:]:
         main_blocks()
     elif "--alpha" in sys.argv[1:]:
         main_alpha()

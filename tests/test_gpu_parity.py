@@ -50,6 +50,35 @@ def test_colour_tables_exhaustive_gpu(dev, golden):
     assert sha(W.ycbcr_to_rgb(ycc)) == meta["kats"]["colour_roundtrip_table_sha256"]
 
 
+def test_colour_helpers_non_uint8_gpu(dev):
+    """rgb_to_ycbcr of float / integer arrays and ycbcr_to_rgb of float16/32/64 arrays
+    (watermarking.py:29, :55): the reference's outputs (tests/golden/helpers.npz), then
+    2^20-pixel random arrays with truncation edges against the oracle."""
+    import os
+
+    from thatsmyface_amd import watermarking as W
+
+    with np.load(os.path.join(os.path.dirname(__file__), "golden", "helpers.npz")) as z:
+        fx = {k: z[k] for k in z.files}
+    for k in sorted(k[3:] for k in fx if k.startswith("in_")):
+        x, want = fx["in_" + k], fx["out_" + k]
+        got = W.rgb_to_ycbcr(x) if k.startswith("fwd_") else W.ycbcr_to_rgb(x)
+        assert got.dtype == want.dtype and np.array_equal(got.view(np.uint8), want.view(np.uint8)), k
+
+    rng = np.random.default_rng(7)
+    rgb = rng.uniform(-20, 280, (1024, 1024, 3)).astype(np.float32)
+    rgb[::7] = np.round(rgb[::7])  # integral values (the uint8 kernel's domain) too
+    got, want = W.rgb_to_ycbcr(rgb), O.rgb_to_ycbcr(rgb)
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+    ycc = rng.uniform(-0.3, 1.3, (1024, 1024, 3))
+    y = (np.arange(1 << 20) % 256) / 255.0
+    ycc[::3, :, 0] = (y.reshape(1024, 1024)[::3] + rng.choice([-1e-9, 0, 1e-9], (342, 1024)))  # truncation edges
+    ycc[::3, :, 1:] = 0.5
+    for dt in (np.float64, np.float32, np.float16):
+        a = ycc.astype(dt)
+        assert np.array_equal(W.ycbcr_to_rgb(a), O.ycbcr_to_rgb(a)), dt
+
+
 ALL_B = [4, 6, 8, 10, 12, 14, 16]  # the app's block-size slider (embed_watermark_page.py:324-331)
 
 

@@ -49,8 +49,10 @@ def test_embed_tiny_image_raises_like_reference():
 
 
 def test_helper_input_checks():
-    with pytest.raises(TypeError):
-        W.rgb_to_ycbcr(np.zeros((2, 2, 3), np.float32))
+    with pytest.raises(ValueError):
+        W.rgb_to_ycbcr(np.zeros((2, 2), np.float32))
+    with pytest.raises(TypeError):  # the reference's in-place "-= 0.5" (:58) refuses integers
+        W.ycbcr_to_rgb(np.zeros((2, 2, 3), np.uint8))
     with pytest.raises(NotImplementedError):
         W.apply_dct_to_block(np.zeros((8, 8), np.float64))
     with pytest.raises(NotImplementedError):

@@ -14,7 +14,7 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # TMFWM_LIB selects an alternative build (e.g. the phase-profile libtmfwm_stamps.so)
 LIB_PATH = os.environ.get("TMFWM_LIB") or os.path.join(_HERE, "libtmfwm.so")
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 MEM_HOST = 0
 MEM_DEVICE = 1
@@ -25,6 +25,10 @@ ERR_HIP = -5
 ERR_UNSUPPORTED = -95
 ERR_NODEVICE = -19
 ERR_NODATA = -61
+
+DT_F16 = 1
+DT_F32 = 2
+DT_F64 = 3
 
 _u8p = ctypes.c_void_p
 _I64 = ctypes.c_int64
@@ -45,6 +49,8 @@ SIGNATURES = {
     "tmfwm_extract_multi": (ctypes.c_int, [_VP, _VP, _I64, _I32, _I32, _I64, _I32, _D, _VP, _VP, _I32, _VP]),
     "tmfwm_rgb_to_ycbcr": (ctypes.c_int, [_VP, _I64, _VP, _I32, _VP]),
     "tmfwm_ycbcr_to_rgb": (ctypes.c_int, [_VP, _I64, _VP, _I32, _VP]),
+    "tmfwm_rgb_to_ycbcr_f32": (ctypes.c_int, [_VP, _I64, _VP, _I32, _VP]),
+    "tmfwm_ycbcr_to_rgb_typed": (ctypes.c_int, [_VP, _I32, _I64, _VP, _I32, _VP]),
     "tmfwm_dct2d_blocks": (ctypes.c_int, [_VP, _I64, _I32, _I32, _I32, _VP]),
     "tmfwm_svd_blocks": (ctypes.c_int, [_VP, _I64, _I32, _VP, _VP, _VP, _VP, _I32, _VP]),
     "tmfwm_lapack_svd_blocks": (ctypes.c_int, [_VP, _I64, _I32, _VP, _VP, _VP, _I32, _I32, _VP]),

@@ -431,7 +431,14 @@ int tmfwm_extract(const uint8_t *wm_rgb, const uint8_t *orig_rgb, int64_t n_fram
                             hip_stream, nullptr);
 }
 
-int tmfwm_rgb_to_ycbcr(const uint8_t *rgb, int64_t npix, float *ycc, int32_t mem_kind, void *hip_stream)
+extern "C++" {
+namespace {
+
+// One elementwise colour helper: in_bytes / out_bytes per pixel; launch(in, out, st)
+// on device pointers.  Host calls stage through library-pool memory.
+template <typename Launch>
+int colour_helper(const void *in, int64_t npix, size_t in_px, void *out, size_t out_px, int32_t mem_kind, void *hip_stream,
+                  Launch launch)
 {
     t_err.clear();
     if (npix < 0) return fail(TMFWM_ERR_INVALID, "npix < 0");
@@ -439,44 +446,64 @@ int tmfwm_rgb_to_ycbcr(const uint8_t *rgb, int64_t npix, float *ycc, int32_t mem
     if (int rc = need_device()) return rc;
     hipStream_t st = pick_stream(hip_stream);
     if (mem_kind == TMFWM_MEM_DEVICE) {
-        if (int rc = check_device_ptr(rgb, "rgb")) return rc;
-        if (int rc = check_device_ptr(ycc, "ycc")) return rc;
-        TMF_HIP(tmf::launch_rgb_to_ycbcr(rgb, npix, ycc, st));
+        if (int rc = check_device_ptr(in, "input")) return rc;
+        if (int rc = check_device_ptr(out, "output")) return rc;
+        TMF_HIP(launch(in, out, st));
         return 0;
     }
-    if (mem_kind != TMFWM_MEM_HOST || !rgb || !ycc) return fail(TMFWM_ERR_INVALID, "bad host arguments");
-    DevBuf di, dy;
-    if (int rc = di.alloc((size_t)npix * 3, st, "rgb")) return rc;
-    if (int rc = dy.alloc((size_t)npix * 12, st, "ycc")) return rc;
-    TMF_HIP(hipMemcpyAsync(di.p, rgb, (size_t)npix * 3, hipMemcpyHostToDevice, st));
-    TMF_HIP(tmf::launch_rgb_to_ycbcr(static_cast<const uint8_t *>(di.p), npix, static_cast<float *>(dy.p), st));
-    TMF_HIP(hipMemcpyAsync(ycc, dy.p, (size_t)npix * 12, hipMemcpyDeviceToHost, st));
+    if (mem_kind != TMFWM_MEM_HOST || !in || !out) return fail(TMFWM_ERR_INVALID, "bad host arguments");
+    DevBuf di, dout;
+    if (int rc = di.alloc((size_t)npix * in_px, st, "input pixels")) return rc;
+    if (int rc = dout.alloc((size_t)npix * out_px, st, "output pixels")) return rc;
+    TMF_HIP(hipMemcpyAsync(di.p, in, (size_t)npix * in_px, hipMemcpyHostToDevice, st));
+    TMF_HIP(launch(di.p, dout.p, st));
+    TMF_HIP(hipMemcpyAsync(out, dout.p, (size_t)npix * out_px, hipMemcpyDeviceToHost, st));
     TMF_HIP(hipStreamSynchronize(st));
     return 0;
 }
 
+size_t dtype_bytes(int32_t dtype)
+{
+    switch (dtype) {
+    case TMFWM_DT_F16: return 2;
+    case TMFWM_DT_F32: return 4;
+    case TMFWM_DT_F64: return 8;
+    default: return 0;
+    }
+}
+
+}  // namespace
+}  // extern "C++"
+
+int tmfwm_rgb_to_ycbcr(const uint8_t *rgb, int64_t npix, float *ycc, int32_t mem_kind, void *hip_stream)
+{
+    return colour_helper(rgb, npix, 3, ycc, 12, mem_kind, hip_stream, [npix](const void *i, void *o, hipStream_t st) {
+        return tmf::launch_rgb_to_ycbcr(static_cast<const uint8_t *>(i), npix, static_cast<float *>(o), st);
+    });
+}
+
+int tmfwm_rgb_to_ycbcr_f32(const float *rgb, int64_t npix, float *ycc, int32_t mem_kind, void *hip_stream)
+{
+    return colour_helper(rgb, npix, 12, ycc, 12, mem_kind, hip_stream, [npix](const void *i, void *o, hipStream_t st) {
+        return tmf::launch_rgb_to_ycbcr_f32(static_cast<const float *>(i), npix, static_cast<float *>(o), st);
+    });
+}
+
+int tmfwm_ycbcr_to_rgb_typed(const void *ycc, int32_t dtype, int64_t npix, uint8_t *rgb, int32_t mem_kind, void *hip_stream)
+{
+    const size_t eb = dtype_bytes(dtype);
+    if (!eb) {
+        t_err.clear();
+        return fail(TMFWM_ERR_INVALID, "dtype %d (TMFWM_DT_F16 / _F32 / _F64)", dtype);
+    }
+    return colour_helper(ycc, npix, 3 * eb, rgb, 3, mem_kind, hip_stream, [npix, dtype](const void *i, void *o, hipStream_t st) {
+        return tmf::launch_ycbcr_to_rgb(i, dtype, npix, static_cast<uint8_t *>(o), st);
+    });
+}
+
 int tmfwm_ycbcr_to_rgb(const float *ycc, int64_t npix, uint8_t *rgb, int32_t mem_kind, void *hip_stream)
 {
-    t_err.clear();
-    if (npix < 0) return fail(TMFWM_ERR_INVALID, "npix < 0");
-    if (npix == 0) return 0;
-    if (int rc = need_device()) return rc;
-    hipStream_t st = pick_stream(hip_stream);
-    if (mem_kind == TMFWM_MEM_DEVICE) {
-        if (int rc = check_device_ptr(ycc, "ycc")) return rc;
-        if (int rc = check_device_ptr(rgb, "rgb")) return rc;
-        TMF_HIP(tmf::launch_ycbcr_to_rgb(ycc, npix, rgb, st));
-        return 0;
-    }
-    if (mem_kind != TMFWM_MEM_HOST || !rgb || !ycc) return fail(TMFWM_ERR_INVALID, "bad host arguments");
-    DevBuf dy, dr;
-    if (int rc = dy.alloc((size_t)npix * 12, st, "ycc")) return rc;
-    if (int rc = dr.alloc((size_t)npix * 3, st, "rgb")) return rc;
-    TMF_HIP(hipMemcpyAsync(dy.p, ycc, (size_t)npix * 12, hipMemcpyHostToDevice, st));
-    TMF_HIP(tmf::launch_ycbcr_to_rgb(static_cast<const float *>(dy.p), npix, static_cast<uint8_t *>(dr.p), st));
-    TMF_HIP(hipMemcpyAsync(rgb, dr.p, (size_t)npix * 3, hipMemcpyDeviceToHost, st));
-    TMF_HIP(hipStreamSynchronize(st));
-    return 0;
+    return tmfwm_ycbcr_to_rgb_typed(ycc, TMFWM_DT_F32, npix, rgb, mem_kind, hip_stream);
 }
 
 int tmfwm_dct2d_blocks(float *blocks, int64_t n_blocks, int32_t block, int32_t inverse, int32_t mem_kind, void *hip_stream)

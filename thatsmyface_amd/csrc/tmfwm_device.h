@@ -72,6 +72,68 @@ TMF_DEVI void colour_inv(float y, float cbs, float crs, uint32_t &R, uint32_t &G
 }
 
 // ---------------------------------------------------------------------------
+// The module-level helpers on non-uint8 inputs (the frame kernels above only ever
+// see uint8 pixels).  rgb_to_ycbcr casts any numeric array with np.array(img,
+// float32) (:29; the caller's cast) and divides by 255 in f32; ycbcr_to_rgb runs
+// in the input's own float type T (:55 img.copy(), :58 "-= 0.5" in T, :64 zeros_like
+// -> the f64 dot is stored in T, :70-73 clip, * 255 in T, truncation).
+// ---------------------------------------------------------------------------
+
+// :29-48 for f32 pixel values v (0..255 scale): v / 255.0f is the IEEE divide (the
+// TU keeps HIP's correctly rounded f32 division: no fast-math), then the dgemv rows.
+TMF_DEVI void colour_fwd_f32(float R, float G, float B, float &y, float &cbs, float &crs)
+{
+    const double r = R / 255.0f, g = G / 255.0f, b = B / 255.0f;
+    y = (float)__builtin_fma(0.114, b, __builtin_fma(0.299, r, 0.587 * g));
+    cbs = (float)__builtin_fma(0.5, b, __builtin_fma(-0.169, r, -0.331 * g)) + 0.5f;
+    crs = (float)__builtin_fma(-0.081, b, __builtin_fma(0.5, r, -0.419 * g)) + 0.5f;
+}
+
+// f64 -> f16 with one rounding (numpy's npy_double_to_half): round to odd into f32
+// (24 >= 11 + 2 bits, so the following RNE f32 -> f16 conversion rounds as a direct
+// f64 -> f16 conversion would), then v_cvt_f16_f32.
+TMF_DEVI _Float16 f16_from_f64(double d)
+{
+    float t = (float)d;
+    if ((double)t != d) {
+        uint32_t u = __float_as_uint(t);
+        if (__builtin_fabs((double)t) > __builtin_fabs(d)) u -= 1; // rounded away from zero: step back
+        t = __uint_as_float(u | 1u);
+    }
+    return (_Float16)t;
+}
+
+template <typename T> TMF_DEVI T round_to(double d)
+{
+    if constexpr (std::is_same_v<T, _Float16>) return f16_from_f64(d);
+    else return (T)d;
+}
+
+// :70-73 in T: np.clip(., 0, 1), * 255 (one T multiply; f16 products are correctly
+// rounded like numpy's half arithmetic), astype(uint8) truncation.  A NaN pixel (only
+// reachable from a NaN / inf input) has no defined uint8 in the reference either.
+template <typename T> TMF_DEVI uint32_t u8_from_unit_t(T f)
+{
+    f = f < T(0) ? T(0) : f;
+    f = f > T(1) ? T(1) : f;
+    return (uint32_t)(float)(f * T(255));
+}
+
+// :55-73 for one pixel of a T-typed array.  The dropped dgemv terms are the exact
+// no-ops of colour_inv (zero products whose sign the clip removes).
+template <typename T> TMF_DEVI void colour_inv_t(T y, T cbs, T crs, uint32_t &R, uint32_t &G, uint32_t &B)
+{
+    if constexpr (std::is_same_v<T, float>) {
+        colour_inv(y, cbs, crs, R, G, B);
+    } else {
+        const double Y = (double)y, CB = (double)(T)(cbs - T(0.5)), CR = (double)(T)(crs - T(0.5));
+        R = u8_from_unit_t<T>(round_to<T>(__builtin_fma(1.403, CR, Y)));
+        G = u8_from_unit_t<T>(round_to<T>(__builtin_fma(-0.714, CR, Y + -0.344 * CB)));
+        B = u8_from_unit_t<T>(round_to<T>(Y + 1.773 * CB));
+    }
+}
+
+// ---------------------------------------------------------------------------
 // pocketfft fp32 DCT-II / DCT-III (N3), every even length 4..16, fully unrolled on
 // register arrays.  rfftp radix passes with compile-time (ido, l1).
 // ---------------------------------------------------------------------------

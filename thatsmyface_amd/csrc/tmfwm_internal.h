@@ -5,6 +5,8 @@
 
 #include <vector>
 
+#include "../../include/tmfwm.h"
+
 namespace tmf {
 
 struct EmbedArgs {
@@ -54,7 +56,8 @@ hipError_t launch_embed(const EmbedArgs &a, hipStream_t st);
 hipError_t launch_edges(const uint8_t *src, uint8_t *dst, int64_t nframes, int H, int W, int64_t frame_stride, int block, hipStream_t st);
 hipError_t launch_extract(const ExtractArgs &a, hipStream_t st);
 hipError_t launch_rgb_to_ycbcr(const uint8_t *rgb, int64_t npix, float *ycc, hipStream_t st);
-hipError_t launch_ycbcr_to_rgb(const float *ycc, int64_t npix, uint8_t *rgb, hipStream_t st);
+hipError_t launch_rgb_to_ycbcr_f32(const float *rgb, int64_t npix, float *ycc, hipStream_t st);
+hipError_t launch_ycbcr_to_rgb(const void *ycc, int dtype, int64_t npix, uint8_t *rgb, hipStream_t st); // dtype TMFWM_DT_F16/F32/F64
 hipError_t launch_dct2d_blocks(float *blocks, int64_t nb, int block, int inverse, hipStream_t st);
 // second pass on the dgesdd route (tmfwm_fallback.hip); max_entries bounds the list
 hipError_t launch_embed_fixup(const EmbedArgs &a, const uint32_t *list, const uint32_t *count, int64_t max_entries, hipStream_t st);

@@ -130,12 +130,20 @@ __global__ __launch_bounds__(256) void rgb_to_ycbcr_kernel(const uint8_t *__rest
     ycc[3 * p + 2] = crs;
 }
 
-__global__ __launch_bounds__(256) void ycbcr_to_rgb_kernel(const float *__restrict__ ycc, int64_t npix, uint8_t *__restrict__ rgb)
+__global__ __launch_bounds__(256) void rgb_to_ycbcr_f32_kernel(const float *__restrict__ rgb, int64_t npix, float *__restrict__ ycc)
+{
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= npix) return;
+    colour_fwd_f32(rgb[3 * p], rgb[3 * p + 1], rgb[3 * p + 2], ycc[3 * p], ycc[3 * p + 1], ycc[3 * p + 2]);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void ycbcr_to_rgb_kernel(const T *__restrict__ ycc, int64_t npix, uint8_t *__restrict__ rgb)
 {
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= npix) return;
     uint32_t R8, G8, B8;
-    colour_inv(ycc[3 * p], ycc[3 * p + 1], ycc[3 * p + 2], R8, G8, B8);
+    colour_inv_t<T>(ycc[3 * p], ycc[3 * p + 1], ycc[3 * p + 2], R8, G8, B8);
     rgb[3 * p] = (uint8_t)R8;
     rgb[3 * p + 1] = (uint8_t)G8;
     rgb[3 * p + 2] = (uint8_t)B8;
@@ -363,10 +371,29 @@ hipError_t launch_rgb_to_ycbcr(const uint8_t *rgb, int64_t npix, float *ycc, hip
     return hipGetLastError();
 }
 
-hipError_t launch_ycbcr_to_rgb(const float *ycc, int64_t npix, uint8_t *rgb, hipStream_t st)
+hipError_t launch_rgb_to_ycbcr_f32(const float *rgb, int64_t npix, float *ycc, hipStream_t st)
 {
     if (npix == 0) return hipSuccess;
-    hipLaunchKernelGGL(ycbcr_to_rgb_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, st, ycc, npix, rgb);
+    hipLaunchKernelGGL(rgb_to_ycbcr_f32_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, st, rgb, npix, ycc);
+    return hipGetLastError();
+}
+
+hipError_t launch_ycbcr_to_rgb(const void *ycc, int dtype, int64_t npix, uint8_t *rgb, hipStream_t st)
+{
+    if (npix == 0) return hipSuccess;
+    const dim3 grid((unsigned)((npix + 255) / 256));
+    switch (dtype) {
+    case TMFWM_DT_F16:
+        hipLaunchKernelGGL(ycbcr_to_rgb_kernel<_Float16>, grid, dim3(256), 0, st, static_cast<const _Float16 *>(ycc), npix, rgb);
+        break;
+    case TMFWM_DT_F32:
+        hipLaunchKernelGGL(ycbcr_to_rgb_kernel<float>, grid, dim3(256), 0, st, static_cast<const float *>(ycc), npix, rgb);
+        break;
+    case TMFWM_DT_F64:
+        hipLaunchKernelGGL(ycbcr_to_rgb_kernel<double>, grid, dim3(256), 0, st, static_cast<const double *>(ycc), npix, rgb);
+        break;
+    default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 

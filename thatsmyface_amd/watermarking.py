@@ -63,36 +63,51 @@ def get_watermark_settings():
     return {"block_size": BLOCK_SIZE, "alpha": ALPHA}
 
 
-def _as_rgb_u8(img) -> np.ndarray:
+def _rgb_pixels(img) -> np.ndarray:
+    """rgb_to_ycbcr's input as the reference reads it (:26-34): PIL -> convert("RGB");
+    uint8 arrays stay uint8 (the fast path), any other numeric array gets the
+    reference's own cast np.array(img, dtype=np.float32) (:29); RGBA -> first three
+    channels (:32-34)."""
     if isinstance(img, Image.Image):
         img = img.convert("RGB")
     arr = np.asarray(img)
+    if arr.dtype != np.uint8:
+        arr = np.asarray(arr, dtype=np.float32)
     if arr.ndim != 3 or arr.shape[-1] not in (3, 4):
         raise ValueError(f"expected an (H, W, 3|4) image, got shape {arr.shape}")
-    if arr.dtype != np.uint8:
-        raise TypeError(f"expected uint8 pixels, got {arr.dtype}")
-    if arr.shape[-1] == 4:  # :32-34 RGBA -> first three channels
+    if arr.shape[-1] == 4:
         arr = arr[..., :3]
     return np.ascontiguousarray(arr)
 
 
 def rgb_to_ycbcr(img) -> np.ndarray:
-    """watermarking.py:23-50 on the GPU: (H, W, 3) float32 (Y, Cb + 0.5, Cr + 0.5)."""
-    rgb = _as_rgb_u8(img)
+    """watermarking.py:23-50 on the GPU: (H, W, 3) float32 (Y, Cb + 0.5, Cr + 0.5).
+    uint8 / PIL inputs go as bytes; other numeric arrays as their float32 cast."""
+    rgb = _rgb_pixels(img)
     out = np.empty(rgb.shape[:2] + (3,), np.float32)
     L = _lib.load()
-    _lib.check(L.tmfwm_rgb_to_ycbcr(_ptr(rgb), rgb.shape[0] * rgb.shape[1], _ptr(out), _lib.MEM_HOST, None), "rgb_to_ycbcr")
+    fn = L.tmfwm_rgb_to_ycbcr if rgb.dtype == np.uint8 else L.tmfwm_rgb_to_ycbcr_f32
+    _lib.check(fn(_ptr(rgb), rgb.shape[0] * rgb.shape[1], _ptr(out), _lib.MEM_HOST, None), "rgb_to_ycbcr")
     return out
 
 
+_YCC_DTYPES = {np.dtype(np.float16): _lib.DT_F16, np.dtype(np.float32): _lib.DT_F32, np.dtype(np.float64): _lib.DT_F64}
+
+
 def ycbcr_to_rgb(img) -> np.ndarray:
-    """watermarking.py:53-73 on the GPU: (H, W, 3) float32 -> (H, W, 3) uint8."""
-    ycc = np.ascontiguousarray(img, dtype=np.float32)
+    """watermarking.py:53-73 on the GPU: (H, W, 3) float16/32/64 -> (H, W, 3) uint8, in
+    the input's own float type as the reference computes (:55 img.copy())."""
+    ycc = np.asarray(img)
+    if ycc.dtype not in _YCC_DTYPES:
+        # the reference's in-place "-= 0.5" (:58) refuses non-float arrays
+        raise TypeError(f"expected a float16/32/64 array, got {ycc.dtype}")
     if ycc.ndim != 3 or ycc.shape[-1] != 3:
         raise ValueError(f"expected an (H, W, 3) array, got shape {ycc.shape}")
+    ycc = np.ascontiguousarray(ycc)
     out = np.empty(ycc.shape, np.uint8)
     L = _lib.load()
-    _lib.check(L.tmfwm_ycbcr_to_rgb(_ptr(ycc), ycc.shape[0] * ycc.shape[1], _ptr(out), _lib.MEM_HOST, None), "ycbcr_to_rgb")
+    _lib.check(L.tmfwm_ycbcr_to_rgb_typed(_ptr(ycc), _YCC_DTYPES[ycc.dtype], ycc.shape[0] * ycc.shape[1], _ptr(out),
+                                          _lib.MEM_HOST, None), "ycbcr_to_rgb")
     return out
 
 
