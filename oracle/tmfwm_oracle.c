@@ -912,7 +912,7 @@ static int jacobi_sweep(double *A, double *V, int b, double c2)
     return rotated;
 }
 
-/* ---- Phase 3 with a Newton finish, b <= 8 -----------------------------
+/* ---- Phase 3 with a Newton finish ---------------------------------------
  * Once a sweep has left only tiny couplings, one first-order Newton step replaces the
  * sweeps that would follow (typically a rotating sweep of tiny angles plus the sweep that
  * finds nothing to rotate).  With V orthogonal to rounding level and A = D V, the step
@@ -927,10 +927,10 @@ static int jacobi_sweep(double *A, double *V, int b, double c2)
  * <= ~2^-24 |X| |F|, is below f64 rounding at that size) and added in f64.  Otherwise
  * the block takes the next sweep.  Per block: sweep; if it rotated nothing, done (the
  * Jacobi's own test); Newton try; repeat (at most JAC_MAX_SWEEPS sweeps). */
-#define NWT_MAX_B 8
 #define NWT_APPLY 7.450580596923828e-09f /* 2^-27 */
-static int g_newton_finish = 1; /* 0: phase 3 = jacobi() for every b (studies only: tools/exp) */
-void orc_set_newton_finish(int on) { g_newton_finish = on; }
+static int g_newton_max_b = ORC_MAXB; /* the Newton finish for b <= this (0: phase 3 = jacobi() for every b) */
+void orc_set_newton_finish(int on) { g_newton_max_b = on ? ORC_MAXB : 0; } /* studies only: tools/exp */
+void orc_set_newton_max_b(int b) { g_newton_max_b = b; }
 
 /* X <- X + f64(f32(X) F) row by row (fma chain over i != j in f32) */
 static void apply_f(double *X, const float *F, int b)
@@ -1002,7 +1002,7 @@ int orc_svd_block_f64(const float *D, int b, double *U, double *sig, double *V)
         return 0;
     }
     /* phase 1: f32 Jacobi on D; phase 2: V0 = Bjorck^2(f64(V32)); phase 3: f64
-     * Jacobi on A0 = D V0 (fma chain over j), accumulating onto V0 (b <= 8: with the
+     * Jacobi on A0 = D V0 (fma chain over j), accumulating onto V0 (with the
      * Newton finish) */
     float A32[ORC_MAXB * ORC_MAXB], V32[ORC_MAXB * ORC_MAXB];
     for (int k = 0; k < b * b; ++k) { A32[k] = D[k]; V32[k] = (k / b == k % b) ? 1.0f : 0.0f; }
@@ -1011,7 +1011,7 @@ int orc_svd_block_f64(const float *D, int b, double *U, double *sig, double *V)
     int sweeps;
     for (int it = 0; it < JAC_BJORCK_STEPS; ++it) bjorck(V, b);
     mul_dv(D, V, A, b);
-    if (b <= NWT_MAX_B && g_newton_finish) sweeps = jacobi_newton(A, V, b) | (s32 << 8);
+    if (b <= g_newton_max_b) sweeps = jacobi_newton(A, V, b) | (s32 << 8);
     else sweeps = jacobi(A, V, b, 1) | (s32 << 8);
     for (int k = 0; k < b; ++k) {
         sig[k] = sqrt(cdot(A + k, A + k, b, b));

@@ -189,10 +189,13 @@ template <int B>
 __global__ __launch_bounds__(64, kEmbedWaves<B>) void embed_kernel(EmbedArgs a)
 {
     constexpr int L = Geo<B>::L, R = Geo<B>::R, BPW = Geo<B>::BPW, LD = B + 1, NW = Geo<B>::NW;
-    __shared__ __attribute__((aligned(16))) float lds[BPW * B * LD];  // also the column norms during the SVD
+    // per-block tile stride: the [B][B+1] transpose tile, or svd3's scratch if larger (8-lane
+    // blocks: the Newton table past the norms / partials), even for 8-byte alignment
+    constexpr int TS = ((B * LD > kScratchFloats<B, L> ? B * LD : kScratchFloats<B, L>) + 1) & ~1;
+    __shared__ __attribute__((aligned(16))) float lds[BPW * TS];  // also svd3's scratch during the SVD
     __shared__ uint32_t pix[R * NW][64];  // this lane's source bytes, parked during the SVD
     const int lane = threadIdx.x & 63, g = lane / L, q = lane % L;
-    float *tile = lds + g * B * LD;
+    float *tile = lds + g * TS;
     const StripPos pos = strip_pos<B>(a.strips_per_row, a.nbw);
     const uint8_t *src = a.src + pos.frame * a.frame_stride;
     uint8_t *dst = a.dst + pos.frame * a.frame_stride;

@@ -1117,12 +1117,11 @@ TMF_DEVI int jacobi(T (&A)[(B + L - 1) / L][B], T (&V)[(B + L - 1) / L][B], int 
     return count;
 }
 
-// ---- Phase 3 with a Newton finish, b <= 8 (oracle jacobi_newton() / newton_try(),
+// ---- Phase 3 with a Newton finish (oracle jacobi_newton() / newton_try(),
 // DESIGN.md 3.4): after each rotating sweep, F_ij = f32(G_ij) / f32(G_jj - G_ii) over the
 // pairs the Jacobi's tests would rotate (G = A^T A); if every |F_ij| <= 2^-27 the block
 // takes V <- V (I + F), A <- A (I + F) -- the correction formed in f32 -- and is done,
 // otherwise it takes the next sweep.
-constexpr int kNewtonMaxB = 8;
 constexpr float kNwtApply = 7.450580596923828e-09f;  // 2^-27
 
 // upper-triangle index of pair (i, j), i < j
@@ -1180,20 +1179,128 @@ TMF_DEVI bool newton_try(double (&A)[(B + L - 1) / L][B], double (&V)[(B + L - 1
     return ok;
 }
 
-// oracle jacobi_newton(): returns sweeps | (Newton steps << 16)
+// The same step for 4- and 8-lane blocks (b = 10..16), whose B(B-1)/2 F values do not fit
+// in registers.  The pairs are visited in the sweep's round order; the lane that would
+// rotate a pair (its owner) forms F_ij from the pair's dot product (8-lane blocks: summed
+// through LDS in the butterfly's order, as kLdsSums) and the diagonal of G (in LDS, as
+// kLdsNorms) and writes it to the block's F table in LDS, slot [round][pair].  If the
+// block takes the step, every lane applies the table to its rows in newton_try()'s order
+// (ascending i; pair (i, j)'s slot is a compile-time function of the schedule).  Same
+// operations on the same values as newton_try(), so the same bits.
+// newton_try_lds scratch (doubles from the block's nl): G at [0, B) (the norm slots), the
+// pair partials at kNwtPart (8-lane blocks: kLdsSums' slots), then (floats) the F table
 template <int B, int L>
-TMF_DEVI int jacobi_newton(double (&A)[(B + L - 1) / L][B], double (&V)[(B + L - 1) / L][B], int q)
+constexpr int kNwtPart = L == 8 ? 32 : B;
+template <int B, int L>
+constexpr int kNwtTable = 2 * (kNwtPart<B, L> + (B / 2) * L);  // float offset of the F table
+template <int B>
+struct PairSlot {  // round and pair index of columns (i, j), i < j, in Sched<B>
+    static constexpr int of(int i, int j)
+    {
+        for (int s = 0; s < B - 1; ++s)
+            for (int p = 0; p < B / 2; ++p)
+                if (Sched<B>::lo(s, p) == i && Sched<B>::hi(s, p) == j) return s * (B / 2) + p;
+        return -1;
+    }
+};
+
+template <int B, int L>
+TMF_DEVI void apply_f_lds(double (&X)[(B + L - 1) / L][B], const float *Ft, bool take)
 {
-    static_assert(B <= kNewtonMaxB, "Newton finish: b <= 8");
+    constexpr int R = kRows<B, L>;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        float xr[B];
+#pragma unroll
+        for (int i = 0; i < B; ++i) xr[i] = (float)X[r][i];
+        static_for<B>([&](auto J) {
+            constexpr int j = J;
+            // the table is read column by column (held in registers it would take B(B-1)/2 VGPRs)
+            lds_order();
+            float acc = 0.0f;
+            static_for<B>([&](auto I) {
+                constexpr int i = I;
+                if constexpr (i < j) acc = __builtin_fmaf(xr[i], Ft[PairSlot<B>::of(i, j)], acc);
+                else if constexpr (i > j) acc = __builtin_fmaf(-xr[i], Ft[PairSlot<B>::of(j, i)], acc);
+            });
+            X[r][j] = take ? X[r][j] + (double)acc : X[r][j];
+        });
+    }
+}
+
+template <int B, int L>
+TMF_DEVI bool newton_try_lds(double (&A)[(B + L - 1) / L][B], double (&V)[(B + L - 1) / L][B], double c2, bool enable, int q,
+                             double *nl)
+{
+    constexpr int R = kRows<B, L>, NP = B / 2, PP = (NP + L - 1) / L;
+    static_assert(L >= 4 && L * PP <= 8, "4- / 8-lane blocks, at most 8 pair slots");
+    double *part = nl + kNwtPart<B, L>;  // partial of pair p from lane k at part[p * L + k]
+    float *Ft = reinterpret_cast<float *>(nl) + kNwtTable<B, L>;  // F of round s, pair p at Ft[s * NP + p]
+    // q through an opaque move: the per-round columns / slots derived from it would
+    // otherwise be hoisted out of the sweep loop and held in registers across it
+    asm volatile("" : "+v"(q));
+    {
+        double G[B];
+        static_for<B>([&](auto K) { G[K] = cdot_part<R, B>(A, K, K); });
+        static_for<B>([&](auto K) { G[K] = group_sum<L>(G[K]); });
+        lds_order();
+        if (q == 0) static_for<B>([&](auto K) { nl[K] = G[K]; });
+        lds_order();
+    }
+    int ok = 1;
+    static_for<B - 1>([&](auto S) {
+        constexpr int s = S;
+        // the rounds are independent (A is not modified): without a fence the scheduler
+        // interleaves them and runs out of registers
+        __builtin_amdgcn_sched_barrier(0);
+        double ga[NP];
+        static_for<NP>([&](auto Pi) { ga[Pi] = cdot_part<R, B>(A, Sched<B>::lo(s, Pi), Sched<B>::hi(s, Pi)); });
+        lds_order();  // after the previous round's reads
+        static_for<NP>([&](auto Pi) { part[Pi * L + q] = ga[Pi]; });
+        lds_order();
+        static_for<PP>([&](auto U) {
+            const int pq = q * PP + U;  // this lane's U-th pair of the round (none if >= NP)
+            const bool has = pq < NP;
+            const int i = (int)__builtin_amdgcn_ubfe(sched_nibbles<B, s, false>(), 4 * pq, 4);
+            const int j = (int)__builtin_amdgcn_ubfe(sched_nibbles<B, s, true>(), 4 * pq, 4);
+            // the butterfly's order (group_sum): ((p0+p1)+(p2+p3)) [+ ((p4+p5)+(p6+p7))]
+            const double *pp = part + (has ? pq : 0) * L;
+            double g = (pp[0] + pp[1]) + (pp[2] + pp[3]);
+            if constexpr (L == 8) g = g + ((pp[4] + pp[5]) + (pp[6] + pp[7]));
+            const double a = nl[i], b = nl[j], g2 = g * g;  // slot 15 (no pair): a dummy read
+            const bool rot = has && !((g2 <= c2 * (a + b)) | (g2 <= (JacP<double>::kTol2 * a) * b));
+            const float f = rot ? (float)g / (float)(b - a) : 0.0f;
+            ok &= (int)(__builtin_fabsf(f) <= kNwtApply);  // NaN / inf fail
+            if (has) Ft[s * NP + pq] = f;
+        });
+    });
+    const bool take = enable && group_or<L>(1 - ok) == 0;
+    if (__any(take)) {
+        lds_order();  // after the owners' table writes
+        apply_f_lds<B, L>(V, Ft, take);
+        apply_f_lds<B, L>(A, Ft, take);
+    }
+    lds_order();  // before the tile's next use
+    return take;
+}
+
+// oracle jacobi_newton(): returns sweeps | (Newton steps << 16).  nl: the block's LDS
+// scratch (b >= 10; see newton_try_lds)
+template <int B, int L>
+TMF_DEVI int jacobi_newton(double (&A)[(B + L - 1) / L][B], double (&V)[(B + L - 1) / L][B], int q, double *nl = nullptr)
+{
     const double c2 = JacP<double>::kC2 * frob2<double, B, L>(A);
     bool active = true;
     int sweeps = 0, newton = 0;
     for (int it = 0; it < JacP<double>::kMaxSweeps; ++it) {
-        const int rotated = jacobi_sweep<double, B, L, true>(A, V, q, nullptr, c2, 0.0, active);
+        const int rotated = jacobi_sweep<double, B, L, true>(A, V, q, nl, c2, 0.0, active);
         sweeps += active ? 1 : 0;
         active = active && group_or<L>(rotated) != 0;
         if (!__any(active)) break;
-        if (newton_try<B, L>(A, V, c2, active)) {
+        bool took;
+        if constexpr (L >= 4) took = newton_try_lds<B, L>(A, V, c2, active, q, nl);
+        else took = newton_try<B, L>(A, V, c2, active);
+        if (took) {
             newton = 1;
             active = false;
         }
@@ -1295,8 +1402,11 @@ struct NoStamp {
     TMF_DEVI void operator()(int) const {}
 };
 
-// nl: this block's LDS scratch for the column norms (kLdsNorms<L>) and the broadcast rotation
-// parameters (kLdsBcast<L>): 32 slots of T, 8-byte aligned
+// nl: this block's LDS scratch for the column norms (kLdsNorms<L>), the broadcast rotation
+// parameters (kLdsBcast<L>), the pair partials (kLdsSums<L>) and the Newton table
+// (newton_try_lds, b >= 10): kScratchFloats<B, L> floats, 8-byte aligned (unused at L <= 2)
+template <int B, int L>
+constexpr int kScratchFloats = L <= 2 ? 2 : kNwtTable<B, L> + (B - 1) * (B / 2);
 template <int B, int L, typename Stamp = NoStamp>
 TMF_DEVI int svd3(const float (&D)[(B + L - 1) / L][B], double (&A)[(B + L - 1) / L][B], double (&V)[(B + L - 1) / L][B], int q,
                   Stamp stamp = {}, void *nl = nullptr)
@@ -1325,8 +1435,7 @@ TMF_DEVI int svd3(const float (&D)[(B + L - 1) / L][B], double (&A)[(B + L - 1) 
     stamp(2);
     lds_order();
     int s64;
-    if constexpr (B <= kNewtonMaxB) s64 = jacobi_newton<B, L>(A, V, q);
-    else s64 = jacobi<double, B, L, true>(A, V, q, static_cast<double *>(nl));
+    s64 = jacobi_newton<B, L>(A, V, q, static_cast<double *>(nl));
     stamp(3);
     return s64 | (s32 << 8);
 }

@@ -176,7 +176,8 @@ __global__ __launch_bounds__(64) void svd_blocks_kernel(const float *__restrict_
                                                         float *__restrict__ S, float *__restrict__ Vt, int32_t *__restrict__ sweeps)
 {
     constexpr int L = Geo<B>::L, R = Geo<B>::R, BPW = Geo<B>::BPW;
-    __shared__ double norms[BPW * (L == 8 ? 96 : 32)];  // kLdsNorms: 16 slots per block (slot 15 is the no-pair lanes' dummy); kLdsBcast: 16 more; kLdsSums: 64
+    constexpr int SD = (kScratchFloats<B, L> + 1) / 2;
+    __shared__ double norms[BPW * SD];  // svd3's per-block LDS scratch
     const int lane = threadIdx.x & 63, g = lane / L, q = lane % L;
     const int64_t blk = (int64_t)blockIdx.x * BPW + g;
     const bool valid = blk < nblocks;
@@ -186,7 +187,7 @@ __global__ __launch_bounds__(64) void svd_blocks_kernel(const float *__restrict_
 #pragma unroll
         for (int c = 0; c < B; ++c) x[r][c] = valid && real_row<B>(q, r) ? D[blk * B * B + (q * R + r) * B + c] : 0.0f;
     double A[R][B], V[R][B];
-    int nsw = svd3<B, L>(x, A, V, q, NoStamp{}, norms + g * (L == 8 ? 96 : 32));
+    int nsw = svd3<B, L>(x, A, V, q, NoStamp{}, norms + g * SD);
     double sig[B];
     float Uf[R][B], Vf[R][B];
 #pragma unroll

@@ -1,4 +1,4 @@
-"""Study: phase 3 with the Newton finish (b <= 8, the contract) against the plain f64
+"""Study: phase 3 with the Newton finish (the contract) against the plain f64
 Jacobi to convergence (orc_set_newton_finish(0)), both against the dgesdd route
 (np.linalg.svd's arithmetic).  Per cover class: flagged blocks, unflagged blocks whose
 IDCT output bits differ from the dgesdd route's, and the per-wave maxima (32 blocks of
