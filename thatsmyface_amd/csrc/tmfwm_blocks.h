@@ -215,7 +215,13 @@ __global__ __launch_bounds__(64, kEmbedWaves<B>) void embed_kernel(EmbedArgs a)
     stamp(0);
 
     double A[R][B], V[R][B];
-    svd3<B, L>(x, A, V, q, stamp, tile);  // :195 (SVD); norms in the block's tile (kLdsNorms)
+    // :195 (SVD); svd3's scratch and (b = 16) the parked D in the block's tile.
+    // Parking D frees 32 VGPRs at b = 16 (scratch 264 -> 216 B per lane); at b = 10 / 14 the
+    // allocation without it fits 2 waves per SIMD spill-free and with it does not, at b = 12
+    // it gains nothing.
+    constexpr bool kPark = B == 16;
+    static_assert(!kPark || kParkOff<L> + B * B <= TS, "parked D fits the tile");
+    svd3<B, L, kPark>(x, A, V, q, stamp, tile, tile + kParkOff<L>);
 
     // singular values, U = A / sigma, sort descending (oracle orc_svd_block)
     double sig[B];

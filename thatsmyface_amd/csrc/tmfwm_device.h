@@ -116,7 +116,9 @@ template <typename T> TMF_DEVI uint32_t u8_from_unit_t(T f)
 {
     f = f < T(0) ? T(0) : f;
     f = f > T(1) ? T(1) : f;
-    return (uint32_t)(float)(f * T(255));
+    const T p = f * T(255);
+    if constexpr (std::is_same_v<T, double>) return (uint32_t)p;  // truncate the double itself
+    else return (uint32_t)(float)p;                               // a half converts to f32 exactly
 }
 
 // :55-73 for one pixel of a T-typed array.  The dropped dgemv terms are the exact
@@ -1407,11 +1409,23 @@ struct NoStamp {
 // (newton_try_lds, b >= 10): kScratchFloats<B, L> floats, 8-byte aligned (unused at L <= 2)
 template <int B, int L>
 constexpr int kScratchFloats = L <= 2 ? 2 : kNwtTable<B, L> + (B - 1) * (B / 2);
-template <int B, int L, typename Stamp = NoStamp>
+// PARK (4- / 8-lane blocks): D waits for A0 = D V0 in LDS, at park (the lane's rows,
+// row-major b x b, from kParkOff<L> floats into the block's scratch: past phase 1's
+// parameter slots), instead of in 32-36 registers that the f32 phase needs.
+template <int L>
+constexpr int kParkOff = L == 8 ? 32 : 0;
+template <int B, int L, bool PARK = false, typename Stamp = NoStamp>
 TMF_DEVI int svd3(const float (&D)[(B + L - 1) / L][B], double (&A)[(B + L - 1) / L][B], double (&V)[(B + L - 1) / L][B], int q,
-                  Stamp stamp = {}, void *nl = nullptr)
+                  Stamp stamp = {}, void *nl = nullptr, float *park = nullptr)
 {
     constexpr int R = kRows<B, L>;
+    if constexpr (PARK) {
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            if (q * R + r < B)
+#pragma unroll
+                for (int c = 0; c < B; ++c) park[(q * R + r) * B + c] = D[r][c];
+    }
     int s32;
     {
         float A32[R][B], V32[R][B];
@@ -1431,7 +1445,17 @@ TMF_DEVI int svd3(const float (&D)[(B + L - 1) / L][B], double (&A)[(B + L - 1) 
     stamp(1);
     bjorck<B, L>(V);
     bjorck<B, L>(V);
-    mul_dv<B, L>(D, V, A);
+    if constexpr (PARK) {
+        lds_order();  // read back here, not earlier
+        float Dp[R][B];
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int c = 0; c < B; ++c) Dp[r][c] = q * R + r < B ? park[(q * R + r) * B + c] : 0.0f;
+        mul_dv<B, L>(Dp, V, A);
+    } else {
+        mul_dv<B, L>(D, V, A);
+    }
     stamp(2);
     lds_order();
     int s64;
