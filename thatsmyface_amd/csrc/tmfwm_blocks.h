@@ -191,7 +191,10 @@ __global__ __launch_bounds__(64, kEmbedWaves<B>) void embed_kernel(EmbedArgs a)
     constexpr int L = Geo<B>::L, R = Geo<B>::R, BPW = Geo<B>::BPW, LD = B + 1, NW = Geo<B>::NW;
     // per-block tile stride: the [B][B+1] transpose tile, or svd3's scratch if larger (8-lane
     // blocks: the Newton table past the norms / partials), even for 8-byte alignment
-    constexpr int TS = ((B * LD > kScratchFloats<B, L> ? B * LD : kScratchFloats<B, L>) + 1) & ~1;
+    constexpr bool kPark = B == 16;  // see svd3 below
+    constexpr int TS0 = B * LD > kScratchFloats<B, L> ? B * LD : kScratchFloats<B, L>;
+    constexpr int TS1 = kPark && kParkOff<L> + B * B > TS0 ? kParkOff<L> + B * B : TS0;
+    constexpr int TS = (TS1 + 1) & ~1;
     __shared__ __attribute__((aligned(16))) float lds[BPW * TS];  // also svd3's scratch during the SVD
     __shared__ uint32_t pix[R * NW][64];  // this lane's source bytes, parked during the SVD
     const int lane = threadIdx.x & 63, g = lane / L, q = lane % L;
@@ -219,7 +222,6 @@ __global__ __launch_bounds__(64, kEmbedWaves<B>) void embed_kernel(EmbedArgs a)
     // Parking D frees 32 VGPRs at b = 16 (scratch 264 -> 216 B per lane); at b = 10 / 14 the
     // allocation without it fits 2 waves per SIMD spill-free and with it does not, at b = 12
     // it gains nothing.
-    constexpr bool kPark = B == 16;
     static_assert(!kPark || kParkOff<L> + B * B <= TS, "parked D fits the tile");
     svd3<B, L, kPark>(x, A, V, q, stamp, tile, tile + kParkOff<L>);
 

@@ -7,7 +7,8 @@
 # E8SCHED=<strategy> overrides the machine scheduler of the embed<8> TU (default max-ilp).
 # SRC_SED='<sed script>' compiles the kernel TUs from a copy of the sources edited by that
 # script (e.g. SRC_SED='s/kPowerIters = 6/kPowerIters = 4/'): experiments without switches
-# in the product code.
+# in the product code.  SRC_REV=<git revision> compiles the kernel TUs of that revision
+# instead (e.g. the build before a change, for an A/B on one box).
 set -euo pipefail
 NAME=$1; shift
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
@@ -15,10 +16,14 @@ C=$ROOT/thatsmyface_amd/csrc
 make -s -C "$C" >/dev/null
 T=$(mktemp -d)
 K=$C
-if [ -n "${SRC_SED:-}" ]; then
-  K=$T/src
-  mkdir -p "$K"
+if [ -n "${SRC_REV:-}" ]; then
+  git -C "$ROOT" archive "$SRC_REV" thatsmyface_amd/csrc include | tar -x -C "$T"
+  K=$T/thatsmyface_amd/csrc
+elif [ -n "${SRC_SED:-}" ]; then
+  K=$T/thatsmyface_amd/csrc  # the tree's layout: tmfwm_internal.h includes ../../include/tmfwm.h
+  mkdir -p "$K" "$T/include"
   cp "$C"/*.h "$C"/*.hip "$K"/
+  cp "$ROOT"/include/*.h "$T/include/"
   sed -i "$SRC_SED" "$K"/*.h "$K"/*.hip
 fi
 F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -fno-slp-vectorize -Wall $*"
