@@ -17,6 +17,11 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "_build", "libtmfwm_oracle.so")
 _lib = None
+# gfx950 v_rsq_f32 truth table (phase 1 of the Jacobi route, tmfwm_oracle.c rsq_hw): deltas in
+# ulps against f32(1 / sqrt(f64(x))) on the 2^24 canonical inputs, measured on the GPU by
+# tools/trans_table.py
+_TRANS_NPZ = os.path.join(os.path.dirname(_HERE), "tests", "golden", "gfx950_trans_delta.npz")
+_rsq_delta = None
 
 _u8p = ctypes.POINTER(ctypes.c_uint8)
 _f32p = ctypes.POINTER(ctypes.c_float)
@@ -63,6 +68,7 @@ def lib():
             "orc_embed_frame_mode": (I32, [_u8p, I32, I32, _u8p, I32, D, _u8p, I32, I32, ctypes.POINTER(I64)]),
             "orc_extract_frame_mode": (I32, [_u8p, _u8p, I32, I32, I32, D, _u8p, I32, I32]),
             "orc_svd_flag": (I32, [_f64p, I32]),
+            "orc_rsq_hw": (ctypes.c_float, [ctypes.c_float]),
             "orc_svd_blocks_f64": (None, [_f32p, I64, I32, _f64p, _f64p, _f64p, I32]),
             "orc_lp_dnrm2": (D, [I32, _f64p, I32]),
             "orc_lp_svd_blocks": (I32, [_f32p, I64, I32, _f32p, _f32p, _f32p, I32]),
@@ -72,6 +78,14 @@ def lib():
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
+        global _rsq_delta
+        with np.load(_TRANS_NPZ) as z:
+            _rsq_delta = np.ascontiguousarray(z["rsq"], dtype=np.int8)
+        if _rsq_delta.shape != (1 << 24,):
+            raise RuntimeError(f"{_TRANS_NPZ}: rsq table has shape {_rsq_delta.shape}")
+        L.orc_set_rsq_table.restype = None
+        L.orc_set_rsq_table.argtypes = [ctypes.c_void_p]
+        L.orc_set_rsq_table(_rsq_delta.ctypes.data)
         _lib = L
     return _lib
 

@@ -120,6 +120,22 @@ def test_svd_blocks_gpu_bit_identical(dev, b):
     assert np.array_equal(sw.cpu().numpy(), swo)
 
 
+@pytest.mark.parametrize("b", [8, 16])
+def test_svd_blocks_gpu_bit_identical_noise_frame(dev, b):
+    """A whole 1080p noise frame of blocks (the bench's cover class): phase 1 runs the
+    hardware v_rsq_f32 on ~10^6 rotations here, modelled in the oracle by its truth table
+    (tests/test_trans_table.py), so every factor bit depends on the model being exact."""
+    from thatsmyface_amd import batch
+
+    Y = O.rgb_to_ycbcr(_u8(90 + b, (1080, 1920, 3)))[..., 0]
+    D = O.dct2d_blocks(_blocks_of(Y, b))
+    U, S, Vt, sw = batch.svd_blocks(torch.from_numpy(D).to(dev))
+    Uo, So, Vo, swo = O.svd_blocks(D)
+    for x, y in ((S, So), (U, Uo), (Vt, Vo)):
+        assert np.array_equal(x.cpu().numpy().view(np.uint32), y.view(np.uint32))
+    assert np.array_equal(sw.cpu().numpy(), swo)
+
+
 # ---------------------------------------------------------------- the dgesdd route on the GPU
 def test_lapack_nrm2_gpu(dev):
     """OpenBLAS's x87 dnrm2 (emulated in integer arithmetic) vs the oracle's long double."""

@@ -713,8 +713,11 @@ TMF_DEVI void static_for(F &&f)
 // ---- cross-lane moves inside a block group (DPP / ds_swizzle, no LDS traffic)
 // DPP controls: quad_perm [1,0,3,2] = 0xB1 (xor 1), [2,3,0,1] = 0x4E (xor 2),
 // row_half_mirror = 0x141 (lane i <-> 7-i within 8 lanes).
+// (update_dpp with bound_ctrl: every control used here reads a valid lane, so the same
+// value as a plain DPP move, and the compiler can fold the move into the f32 add or
+// subtract that consumes it: v_add_f32_dpp)
 template <int CTRL>
-TMF_DEVI int dpp_i(int v) { return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, false); }
+TMF_DEVI int dpp_i(int v) { return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, true); }
 template <int PATTERN>
 TMF_DEVI int swz_i(int v) { return __builtin_amdgcn_ds_swizzle(v, PATTERN); }
 
@@ -821,8 +824,11 @@ TMF_DEVI float blend(int mask, float x, float y)
     return __builtin_bit_cast(float, (xb & mask) | (yb & ~mask));
 }
 
-// 1/sqrt(x) from IEEE ops only (oracle rsqrt_n / rsqrtf_n): integer seed + Newton
-TMF_DEVI double rsqrt_n(double x)
+// 1/sqrt(x) of the contract.  f64 phase: IEEE ops only (oracle rsqrt_n),
+// integer seed + 4 Newton steps.  f32 phase (a preconditioner): the hardware v_rsq_f32,
+// which the oracle models by its measured truth table (oracle rsq_hw,
+// tests/golden/gfx950_trans_delta.npz).
+TMF_DEVI double rsqrt_c(double x)
 {
     const unsigned long long i = 0x5fe6eb50c7b537a9ull - (__builtin_bit_cast(unsigned long long, x) >> 1);
     double y = __builtin_bit_cast(double, i);
@@ -835,19 +841,7 @@ TMF_DEVI double rsqrt_n(double x)
     }
     return y;
 }
-TMF_DEVI float rsqrt_n(float x)
-{
-    const unsigned i = 0x5f375a86u - (__builtin_bit_cast(unsigned, x) >> 1);
-    float y = __builtin_bit_cast(float, i);
-    const float hx = 0.5f * x;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        const float t = y * y;
-        const float u = __builtin_fmaf(-hx, t, 1.5f);
-        y = y * u;
-    }
-    return y;
-}
+TMF_DEVI float rsqrt_c(float x) { return __builtin_amdgcn_rsqf(x); }
 
 // Columns i, j of A (and V) <- (c x - s y, s x + c y) as fma(-s, y, c*x), fma(s, x, c*y)
 template <int R, int B, bool WANT_V, typename T>
@@ -882,9 +876,9 @@ TMF_DEVI Rot<T> rotation(T alpha, T beta, T gamma)
     const T d = beta - alpha;
     const T g = gamma + gamma;
     const T x = fma_t(d, d, g * g);
-    const T r = x * rsqrt_n(x);
+    const T r = x * rsqrt_c(x);
     const T w = abs_t(d) + r;
-    const T q = rsqrt_n((r + r) * w);
+    const T q = rsqrt_c((r + r) * w);
     const T sg = sign1_t(d);
     o.c = w * q;
     o.s = (g * sg) * q;
