@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define TMFWM_ABI_VERSION 5
+#define TMFWM_ABI_VERSION 6
 
 #define TMFWM_MEM_HOST 0
 #define TMFWM_MEM_DEVICE 1
@@ -58,6 +58,12 @@ int tmfwm_abi_version(void);
 
 /* Message of the last failed call on this thread ("" if none). */
 const char *tmfwm_last_error(void);
+
+/* Work report of the last tmfwm_embed_ex / tmfwm_extract_ex call on this thread that asked
+ * for one (non-NULL n_lapack_blocks): the number of blocks embed's strip pass left to its
+ * list pass (blocks needing more f64 Jacobi sweeps than the rest of their wave),
+ * 0 for extract; -1 before any such call.  Diagnostics only: the pixels do not depend on it. */
+int64_t tmfwm_last_list_pass_blocks(void);
 
 /* Number of visible HIP devices (0 when none); never fails. */
 int tmfwm_device_count(void);

@@ -384,6 +384,30 @@ def test_chunked_second_pass_vs_oracle(dev, monkeypatch):
         assert np.array_equal(ext1[f].cpu().numpy(), O.extract_frame(ref, host[f], b, 0.1)), f
 
 
+def test_list_pass_vs_oracle(dev):
+    """embed's list pass: at b = 8 a wave whose last <= 4 unfinished blocks
+    need another f64 sweep leaves them to the list pass.  Noise covers (1 % of blocks) and
+    camera-like covers (nearly every block needs 2 sweeps, a few 3) both take it; the pixels
+    equal the oracle's and a run with the list pass equals itself under chunking."""
+    import sys
+
+    from golden.gen_golden import wmark
+
+    from thatsmyface_amd import batch
+
+    sys.path.insert(0, str(__import__("pathlib").Path(__file__).resolve().parents[1] / "tools" / "exp"))
+    from flag_margin import photo_cover
+
+    b, H, W = 8, 544, 960
+    host = np.stack([_u8(71, (H, W, 3)), photo_cover(H, W, 5), _u8(72, (H, W, 3)), photo_cover(H, W, 6)])
+    t = wmark("qr", H // b, W // b, 9)
+    st = {}
+    out = batch.embed_batch(torch.from_numpy(host).to(dev), torch.from_numpy(t).to(dev), b, 0.1, stats=st)
+    assert st["list_pass_blocks"] > 0, st
+    for f in range(len(host)):
+        assert np.array_equal(out[f].cpu().numpy(), O.embed_frame(host[f], t, b, 0.1)), f
+
+
 @pytest.mark.parametrize("b", [8, 6, 12, 14])
 def test_unaligned_strided_frames(dev, b):
     """Frames at odd byte offsets / strides take the byte-granular load path."""

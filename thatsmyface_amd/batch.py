@@ -64,6 +64,7 @@ def embed_batch(frames: torch.Tensor, wm_tile: torch.Tensor, block: int = 8, alp
                                     out.data_ptr(), _lib.MEM_DEVICE, _stream(stream), ptr), "embed_batch")
     if stats is not None:
         stats["lapack_blocks"] = int(cnt.value)
+        stats["list_pass_blocks"] = int(L.tmfwm_last_list_pass_blocks())
     return out
 
 

@@ -185,21 +185,38 @@ TMF_DEVI void luma_rows(const uint32_t (&words)[Geo<B>::R][Geo<B>::NW], float (&
 template <int B>
 constexpr int kEmbedWaves = (B == 12 || B == 16) ? 2 : 1;
 
+// Strip pass: once at most kDeferMax blocks of a wave still need f64 sweeps after a sweep
+// and its Newton try, the wave leaves them to the list pass instead of running another
+// sweep for them (they write nothing here; the list pass redoes them from their pixels with
+// the whole loop).  On noise covers at b = 8, 1 % of blocks need a second sweep and 26 % of
+// waves would run one for them; on photo-like covers nearly every block needs two, and the
+// waves keep going as before.
 template <int B>
-__global__ __launch_bounds__(64, kEmbedWaves<B>) void embed_kernel(EmbedArgs a)
+constexpr int kDeferMax = B == 8 ? 4 : 0;
+constexpr unsigned kListPassGrid = 2048;  // waves of the list pass (2 per SIMD fill the chip)
+
+// b = 16 parks D in LDS during phase 1 (svd3, PARK): frees 32 VGPRs (scratch 264 -> 216 B
+// per lane); at b = 10 / 14 the allocation without it fits 2 waves per SIMD spill-free and
+// with it does not, at b = 12 it gains nothing
+template <int B>
+constexpr bool kParkD = B == 16;
+// per-block LDS tile stride (floats): the [B][B+1] transpose tile, or svd3's scratch if larger
+// (8-lane blocks: the Newton table past the norms / partials; b = 16: the parked D past
+// phase 1's parameter slots), even for 8-byte alignment
+template <int B>
+constexpr int kEmbedTS0 = B * (B + 1) > kScratchFloats<B, Geo<B>::L> ? B * (B + 1) : kScratchFloats<B, Geo<B>::L>;
+template <int B>
+constexpr int kEmbedTS = ((kParkD<B> && kParkOff<Geo<B>::L> + B * B > kEmbedTS0<B> ? kParkOff<Geo<B>::L> + B * B : kEmbedTS0<B>) + 1) & ~1;
+
+// One wave's blocks: strip mode (LIST = false: the strip of blockIdx) or list mode (pos and
+// id from the slow list).  id = (frame * nbh + bi) * nbw + bj, relative to a.src.
+template <int B, bool LIST>
+TMF_DEVI void embed_blocks(const EmbedArgs &a, const StripPos &pos, uint32_t id, float *lds, uint32_t (*pix)[64])
 {
-    constexpr int L = Geo<B>::L, R = Geo<B>::R, BPW = Geo<B>::BPW, LD = B + 1, NW = Geo<B>::NW;
-    // per-block tile stride: the [B][B+1] transpose tile, or svd3's scratch if larger (8-lane
-    // blocks: the Newton table past the norms / partials), even for 8-byte alignment
-    constexpr bool kPark = B == 16;  // see svd3 below
-    constexpr int TS0 = B * LD > kScratchFloats<B, L> ? B * LD : kScratchFloats<B, L>;
-    constexpr int TS1 = kPark && kParkOff<L> + B * B > TS0 ? kParkOff<L> + B * B : TS0;
-    constexpr int TS = (TS1 + 1) & ~1;
-    __shared__ __attribute__((aligned(16))) float lds[BPW * TS];  // also svd3's scratch during the SVD
-    __shared__ uint32_t pix[R * NW][64];  // this lane's source bytes, parked during the SVD
+    constexpr int L = Geo<B>::L, R = Geo<B>::R, LD = B + 1, NW = Geo<B>::NW, TS = kEmbedTS<B>;
+    constexpr bool kPark = kParkD<B>;
     const int lane = threadIdx.x & 63, g = lane / L, q = lane % L;
     float *tile = lds + g * TS;
-    const StripPos pos = strip_pos<B>(a.strips_per_row, a.nbw);
     const uint8_t *src = a.src + pos.frame * a.frame_stride;
     uint8_t *dst = a.dst + pos.frame * a.frame_stride;
 
@@ -218,12 +235,11 @@ __global__ __launch_bounds__(64, kEmbedWaves<B>) void embed_kernel(EmbedArgs a)
     stamp(0);
 
     double A[R][B], V[R][B];
-    // :195 (SVD); svd3's scratch and (b = 16) the parked D in the block's tile.
-    // Parking D frees 32 VGPRs at b = 16 (scratch 264 -> 216 B per lane); at b = 10 / 14 the
-    // allocation without it fits 2 waves per SIMD spill-free and with it does not, at b = 12
-    // it gains nothing.
+    // :195 (SVD); svd3's scratch and (b = 16) the parked D in the block's tile
     static_assert(!kPark || kParkOff<L> + B * B <= TS, "parked D fits the tile");
-    svd3<B, L, kPark>(x, A, V, q, stamp, tile, tile + kParkOff<L>);
+    bool slow = false;  // strip pass: this block was left to the list pass
+    svd3<B, L, kPark>(x, A, V, q, stamp, tile, tile + kParkOff<L>, !LIST && a.slow_list ? kDeferMax<B> : 0, &slow);
+    if (slow && pos.valid && q == 0) a.slow_list[atomicAdd(a.slow_count, 1u)] = id;
 
     // singular values, U = A / sigma, sort descending (oracle orc_svd_block)
     double sig[B];
@@ -262,8 +278,7 @@ __global__ __launch_bounds__(64, kEmbedWaves<B>) void embed_kernel(EmbedArgs a)
         double m = s1;
 #pragma unroll
         for (int k = 0; k < B; ++k) m = ((float)sig[k] != 0.0f && g[k] < m) ? g[k] : m;
-        if (m * 1048576.0 < s1 && pos.valid && q == 0)
-            a.fb_list[atomicAdd(a.fb_count, 1u)] = (uint32_t)(((int64_t)blockIdx.y * a.nbh + pos.bi) * a.nbw + pos.bj);
+        if (m * 1048576.0 < s1 && pos.valid && !slow && q == 0) a.fb_list[atomicAdd(a.fb_count, 1u)] = id;
     }
     bool zero = true;
 #pragma unroll
@@ -335,7 +350,7 @@ __global__ __launch_bounds__(64, kEmbedWaves<B>) void embed_kernel(EmbedArgs a)
     stamp(5);
 
     // :207-216 write back and ycbcr_to_rgb with this lane's original chroma
-    if (pos.valid) {
+    if (pos.valid && !slow) {
         uint32_t words[R][NW];
 #pragma unroll
         for (int r = 0; r < R; ++r)
@@ -363,6 +378,34 @@ __global__ __launch_bounds__(64, kEmbedWaves<B>) void embed_kernel(EmbedArgs a)
         }
     }
     stamp(6);
+}
+
+template <int B, bool LIST = false>
+__global__ __launch_bounds__(64, kEmbedWaves<B>) void embed_kernel(EmbedArgs a)
+{
+    constexpr int L = Geo<B>::L, R = Geo<B>::R, BPW = Geo<B>::BPW, NW = Geo<B>::NW, TS = kEmbedTS<B>;
+    __shared__ __attribute__((aligned(16))) float lds[BPW * TS];  // also svd3's scratch during the SVD
+    __shared__ uint32_t pix[R * NW][64];  // this lane's source bytes, parked during the SVD
+    if constexpr (LIST) {
+        // grid-stride over the slow list (its length is known on the device only)
+        const uint32_t n = *a.slow_count, per_frame = (uint32_t)a.nbh * (uint32_t)a.nbw;
+        const int g = (threadIdx.x & 63) / L;
+        for (uint32_t t0 = blockIdx.x * BPW; t0 < n; t0 += gridDim.x * BPW) {
+            StripPos pos;
+            pos.valid = t0 + g < n;
+            const uint32_t id = pos.valid ? a.slow_list[t0 + g] : 0u;
+            pos.frame = id / per_frame;
+            const uint32_t rem = id % per_frame;
+            pos.bi = (int)(rem / (uint32_t)a.nbw);
+            pos.bj = (int)(rem % (uint32_t)a.nbw);
+            embed_blocks<B, true>(a, pos, id, lds, pix);
+            __syncthreads();  // the LDS tiles are reused by the next listed blocks
+        }
+    } else {
+        const StripPos pos = strip_pos<B>(a.strips_per_row, a.nbw);
+        const uint32_t id = (uint32_t)(((int64_t)blockIdx.y * a.nbh + pos.bi) * a.nbw + pos.bj);
+        embed_blocks<B, false>(a, pos, id, lds, pix);
+    }
 }
 
 }  // namespace tmf

@@ -18,6 +18,7 @@
 namespace {
 
 thread_local std::string t_err;
+thread_local int64_t t_list_pass = -1;  // tmfwm_last_list_pass_blocks
 
 int fail(int code, const char *fmt, ...)
 {
@@ -184,21 +185,23 @@ struct Chunks {
 };
 
 // copy the per-chunk counts back (synchronises the stream) and sum them; dcounts holds the
-// chunks' dgesdd-route counts, then their non-convergence counts
+// chunks' dgesdd-route counts, then their non-convergence counts, then their list-pass counts
 int sum_counts(const uint32_t *dcounts, int64_t nchunks, hipStream_t st, int64_t *out)
 {
-    std::vector<uint32_t> h((size_t)(2 * nchunks));
+    std::vector<uint32_t> h((size_t)(3 * nchunks));
     if (nchunks) {
-        hipError_t e = hipMemcpyAsync(h.data(), dcounts, (size_t)nchunks * 8, hipMemcpyDeviceToHost, st);
+        hipError_t e = hipMemcpyAsync(h.data(), dcounts, (size_t)nchunks * 12, hipMemcpyDeviceToHost, st);
         if (e == hipSuccess) e = hipStreamSynchronize(st);
         if (e != hipSuccess) return fail(TMFWM_ERR_HIP, "reading the dgesdd-route counts failed: %s", hipGetErrorString(e));
     }
-    int64_t t = 0, bad = 0;
+    int64_t t = 0, bad = 0, slow = 0;
     for (int64_t c = 0; c < nchunks; ++c) {
         t += h[(size_t)c];
         bad += h[(size_t)(nchunks + c)];
+        slow += h[(size_t)(2 * nchunks + c)];
     }
     *out = t;
+    t_list_pass = slow;
     if (bad)
         return fail(TMFWM_ERR_HIP, "dgesdd route: dbdsqr did not converge on %lld block(s) (np.linalg.svd raises LinAlgError there)",
                     (long long)bad);
@@ -228,15 +231,21 @@ int run_embed(EmbedArgs a, hipStream_t st, int64_t *n_lapack)
 {
     Chunks ch;
     ch.plan(a.nframes, (int64_t)a.nbh * a.nbw);
-    DevBuf list, counts;
+    DevBuf list, slow, counts;
     if (ch.cap > 0) {
         if (int rc = list.alloc((size_t)ch.cap * 4, st, "dgesdd-route block list")) return rc;
-        if (int rc = counts.alloc((size_t)ch.n * 8, st, "dgesdd-route counts")) return rc;
-        TMF_HIP(hipMemsetAsync(counts.p, 0, (size_t)ch.n * 8, st));
+        if (embed_defers(a.block))
+            if (int rc = slow.alloc((size_t)ch.cap * 4, st, "list-pass block list")) return rc;
+        // per chunk: dgesdd-route count, non-convergence count, list-pass count
+        if (int rc = counts.alloc((size_t)ch.n * 12, st, "block-list counts")) return rc;
+        TMF_HIP(hipMemsetAsync(counts.p, 0, (size_t)ch.n * 12, st));
     }
     if (ch.cap == 0) {  // no full block: colour round trip only
         TMF_HIP(launch_embed(a, st));
-        if (n_lapack) *n_lapack = 0;
+        if (n_lapack) {
+            *n_lapack = 0;
+            t_list_pass = 0;
+        }
         return 0;
     }
     for (int64_t c = 0; c < ch.n; ++c) {
@@ -248,6 +257,8 @@ int run_embed(EmbedArgs a, hipStream_t st, int64_t *n_lapack)
         k.fb_list = static_cast<uint32_t *>(list.p);
         k.fb_count = static_cast<uint32_t *>(counts.p) + c;
         k.fb_bad = static_cast<uint32_t *>(counts.p) + ch.n + c;
+        k.slow_list = static_cast<uint32_t *>(slow.p);  // null unless embed_defers(block)
+        k.slow_count = static_cast<uint32_t *>(counts.p) + 2 * ch.n + c;
         TMF_HIP(launch_embed(k, st));
         TMF_HIP(launch_embed_fixup(k, k.fb_list, k.fb_count, k.nframes * ch.per_frame, st));
     }
@@ -260,13 +271,16 @@ int run_extract(ExtractArgs a, hipStream_t st, int64_t *n_lapack)
     Chunks ch;
     ch.plan(a.nframes, (int64_t)a.nbh * a.nbw);
     if (ch.cap == 0) {
-        if (n_lapack) *n_lapack = 0;
+        if (n_lapack) {
+            *n_lapack = 0;
+            t_list_pass = 0;
+        }
         return 0;
     }
     DevBuf list, counts;
     if (int rc = list.alloc((size_t)ch.cap * 4, st, "dgesdd-route block list")) return rc;
-    if (int rc = counts.alloc((size_t)ch.n * 8, st, "dgesdd-route counts")) return rc;
-    TMF_HIP(hipMemsetAsync(counts.p, 0, (size_t)ch.n * 8, st));
+    if (int rc = counts.alloc((size_t)ch.n * 12, st, "block-list counts")) return rc;  // as run_embed's (no list pass)
+    TMF_HIP(hipMemsetAsync(counts.p, 0, (size_t)ch.n * 12, st));
     for (int64_t c = 0; c < ch.n; ++c) {
         ExtractArgs k = a;
         const int64_t f0 = c * ch.frames;
@@ -290,6 +304,8 @@ extern "C" {
 int tmfwm_abi_version(void) { return TMFWM_ABI_VERSION; }
 
 const char *tmfwm_last_error(void) { return t_err.c_str(); }
+
+int64_t tmfwm_last_list_pass_blocks(void) { return t_list_pass; }
 
 int tmfwm_device_count(void)
 {

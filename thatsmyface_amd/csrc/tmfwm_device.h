@@ -1281,9 +1281,15 @@ TMF_DEVI bool newton_try_lds(double (&A)[(B + L - 1) / L][B], double (&V)[(B + L
 }
 
 // oracle jacobi_newton(): returns sweeps | (Newton steps << 16).  nl: the block's LDS
-// scratch (b >= 10; see newton_try_lds)
+// scratch (b >= 10; see newton_try_lds).  defer_max > 0 (the embed kernel's strip pass,
+// DESIGN.md 4): once no more than defer_max blocks of the wave are still unfinished after a
+// sweep and its Newton try, the wave stops and *unfinished tells each block whether it was
+// one of them -- the list pass redoes those from their pixels with the whole loop, so their
+// bits are those of the uninterrupted loop (a block's arithmetic never depends on the other
+// blocks of its wave).
 template <int B, int L>
-TMF_DEVI int jacobi_newton(double (&A)[(B + L - 1) / L][B], double (&V)[(B + L - 1) / L][B], int q, double *nl = nullptr)
+TMF_DEVI int jacobi_newton(double (&A)[(B + L - 1) / L][B], double (&V)[(B + L - 1) / L][B], int q, double *nl = nullptr,
+                           int defer_max = 0, bool *unfinished = nullptr)
 {
     const double c2 = JacP<double>::kC2 * frob2<double, B, L>(A);
     bool active = true;
@@ -1301,6 +1307,10 @@ TMF_DEVI int jacobi_newton(double (&A)[(B + L - 1) / L][B], double (&V)[(B + L -
             active = false;
         }
         if (!__any(active)) break;
+        if (defer_max > 0 && __builtin_popcountll(__ballot(active && q == 0)) <= defer_max) {
+            if (unfinished) *unfinished = active;
+            break;
+        }
     }
     return sweeps | (newton << 16);
 }
@@ -1410,7 +1420,7 @@ template <int L>
 constexpr int kParkOff = L == 8 ? 32 : 0;
 template <int B, int L, bool PARK = false, typename Stamp = NoStamp>
 TMF_DEVI int svd3(const float (&D)[(B + L - 1) / L][B], double (&A)[(B + L - 1) / L][B], double (&V)[(B + L - 1) / L][B], int q,
-                  Stamp stamp = {}, void *nl = nullptr, float *park = nullptr)
+                  Stamp stamp = {}, void *nl = nullptr, float *park = nullptr, int defer_max = 0, bool *unfinished = nullptr)
 {
     constexpr int R = kRows<B, L>;
     if constexpr (PARK) {
@@ -1453,7 +1463,7 @@ TMF_DEVI int svd3(const float (&D)[(B + L - 1) / L][B], double (&A)[(B + L - 1) 
     stamp(2);
     lds_order();
     int s64;
-    s64 = jacobi_newton<B, L>(A, V, q, static_cast<double *>(nl));
+    s64 = jacobi_newton<B, L>(A, V, q, static_cast<double *>(nl), defer_max, unfinished);
     stamp(3);
     return s64 | (s32 << 8);
 }

@@ -6,7 +6,8 @@
 #include "tmfwm_blocks.h"
 
 namespace tmf {
-template __global__ void embed_kernel<8>(EmbedArgs);
+template __global__ void embed_kernel<8, false>(EmbedArgs);
+template __global__ void embed_kernel<8, true>(EmbedArgs);
 }  // namespace tmf
 
 #ifdef TMF_STAMPS

@@ -23,6 +23,10 @@ struct EmbedArgs {
     uint32_t *fb_list;
     uint32_t *fb_count;
     uint32_t *fb_bad;        // dgesdd-route blocks whose dbdsqr did not converge (may be null)
+    // list pass: blocks the first pass leaves unfinished after its f64 sweep
+    // budget, same ids; null: the first pass runs every block to the end
+    uint32_t *slow_list;
+    uint32_t *slow_count;
 };
 
 struct ExtractArgs {
@@ -53,6 +57,7 @@ void clear_error();
 int check_frames(int64_t n, int32_t H, int32_t W, int64_t stride, int32_t block);
 
 hipError_t launch_embed(const EmbedArgs &a, hipStream_t st);
+bool embed_defers(int block);  // the strip pass of embed_kernel<block> can leave blocks to a list pass
 hipError_t launch_edges(const uint8_t *src, uint8_t *dst, int64_t nframes, int H, int W, int64_t frame_stride, int block, hipStream_t st);
 hipError_t launch_extract(const ExtractArgs &a, hipStream_t st);
 hipError_t launch_rgb_to_ycbcr(const uint8_t *rgb, int64_t npix, float *ycc, hipStream_t st);

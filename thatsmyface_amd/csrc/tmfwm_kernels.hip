@@ -14,7 +14,8 @@
 
 namespace tmf {
 
-extern template __global__ void embed_kernel<8>(EmbedArgs);  // tmfwm_embed8.hip
+extern template __global__ void embed_kernel<8, false>(EmbedArgs);  // tmfwm_embed8.hip
+extern template __global__ void embed_kernel<8, true>(EmbedArgs);
 
 // ---------------------------------------------------------------------------
 // Extract: watermarking.py:241-289 fused; sigma_1 of both images per block.
@@ -287,10 +288,17 @@ static hipError_t launch_embed_b(EmbedArgs a, hipStream_t st)
         const int64_t nf = a.nframes - f0 < 65535 ? a.nframes - f0 : 65535;
         c.src = a.src + f0 * a.frame_stride;
         c.dst = a.dst + f0 * a.frame_stride;
-        hipLaunchKernelGGL(embed_kernel<B>, dim3((unsigned)gx, (unsigned)nf), dim3(64), 0, st, c);
+        hipLaunchKernelGGL((embed_kernel<B, false>), dim3((unsigned)gx, (unsigned)nf), dim3(64), 0, st, c);
+    }
+    if (kDeferMax<B> > 0 && a.slow_list) {  // the list pass over the blocks the first pass left unfinished (ids relative to a.src)
+        const int64_t waves = ((int64_t)a.nframes * a.nbh * a.nbw + Geo<B>::BPW - 1) / Geo<B>::BPW;
+        const unsigned grid = (unsigned)(waves < kListPassGrid ? waves : kListPassGrid);
+        if constexpr (kDeferMax<B> > 0) hipLaunchKernelGGL((embed_kernel<B, true>), dim3(grid), dim3(64), 0, st, a);
     }
     return hipGetLastError();
 }
+
+bool embed_defers(int block) { return block == 8 ? kDeferMax<8> > 0 : false; }
 
 hipError_t launch_embed(const EmbedArgs &a, hipStream_t st)
 {

@@ -16,9 +16,15 @@ CHILD = r'''
 import hashlib, json, os, sys, torch
 sys.path.insert(0, os.environ["ROOT"])
 from thatsmyface_amd import batch
-b, n = int(sys.argv[1]), int(sys.argv[2])
+b, n, kind = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3]
 dev = torch.device("cuda", 0)
-fr = batch.synth_frames(n, 2160, 3840, device=dev)
+if kind == "photo":  # camera-like covers (tools/exp/flag_margin.py), 4 distinct frames repeated
+    sys.path.insert(0, os.path.join(os.environ["ROOT"], "tools", "exp"))
+    from flag_margin import photo_cover
+    ph = torch.stack([torch.from_numpy(photo_cover(2160, 3840, 100 + k)) for k in range(4)]).to(dev)
+    fr = ph.repeat((n + 3) // 4, 1, 1, 1)[:n].contiguous()
+else:
+    fr = batch.synth_frames(n, 2160, 3840, device=dev)
 tile = batch.synth_tile(2160 // b, 3840 // b, device=dev)
 out = batch.embed_batch(fr, tile, b, 0.1)
 ext = batch.extract_batch(out, fr, b, 0.1)
@@ -37,7 +43,8 @@ for name, fn in (("embed", lambda: batch.embed_batch(fr, tile, b, 0.1, out=out))
 se, sx = {}, {}
 batch.embed_batch(fr, tile, b, 0.1, out=out, stats=se)
 batch.extract_batch(out, fr, b, 0.1, out=ext, stats=sx)
-print(json.dumps({"hash": h, "us_per_frame": res, "lapack_blocks": {"embed": se["lapack_blocks"], "extract": sx["lapack_blocks"]}}))
+print(json.dumps({"hash": h, "us_per_frame": res, "lapack_blocks": {"embed": se["lapack_blocks"], "extract": sx["lapack_blocks"]},
+                  "list_pass_blocks": se.get("list_pass_blocks")}))
 '''
 
 
@@ -46,6 +53,7 @@ def main():
     p.add_argument("--block", type=int, default=8)
     p.add_argument("--frames", type=int, default=64)
     p.add_argument("--rounds", type=int, default=3)
+    p.add_argument("--cover", choices=("noise", "photo"), default="noise")
     p.add_argument("names", nargs="+")
     a = p.parse_args()
     res = {n: [] for n in a.names}
@@ -53,7 +61,7 @@ def main():
     for r in range(a.rounds):
         for n in a.names:
             env = dict(os.environ, ROOT=ROOT, TMFWM_LIB=os.path.join(ROOT, "variants", f"libtmfwm_{n}.so"))
-            out = subprocess.run([sys.executable, "-c", CHILD, str(a.block), str(a.frames)], env=env, capture_output=True,
+            out = subprocess.run([sys.executable, "-c", CHILD, str(a.block), str(a.frames), a.cover], env=env, capture_output=True,
                                  text=True, timeout=300)
             if out.returncode != 0:
                 print(json.dumps({"variant": n, "error": out.stderr[-2000:]}), flush=True)
