@@ -22,15 +22,17 @@ namespace tmf {
 // Colour (N1, N2, N9)
 // ---------------------------------------------------------------------------
 
-// f32(v) / 255.0f, correctly rounded (watermarking.py:29), as one multiply plus a
-// residual correction; exhaustively equal to the IEEE divide for v = 0..255.
+// f32(v) / 255.0f, correctly rounded (watermarking.py:29), as fma(x, H, x * Lo) with
+// 1/255 = H + Lo split into two floats: x*H is exact inside the fma and x*Lo's rounding is
+// ~2^-48 relative, far below the distance of any v/255 from an f32 rounding boundary --
+// exhaustively equal to the IEEE divide for v = 0..255 (tests/test_host_api.py).  Two
+// operations instead of a multiply and a two-fma residual correction.
+constexpr float kUnitHi = 0.003921568859368562698f;    // f32(1/255)
+constexpr float kUnitLo = -2.3191758e-10f;             // f32(1/255 - kUnitHi)
 TMF_DEVI float unit_from_u8(uint32_t v)
 {
     const float x = (float)v;
-    constexpr float r = 1.0f / 255.0f;
-    const float q = x * r;
-    const float e = __builtin_fmaf(-q, 255.0f, x);
-    return __builtin_fmaf(e, r, q);
+    return __builtin_fmaf(x, kUnitHi, x * kUnitLo);
 }
 
 // Y only (watermarking.py:37-45, row 0 of the transform; OpenBLAS dgemv FMA pattern)
@@ -1148,7 +1150,41 @@ TMF_DEVI void apply_f(double (&X)[(B + L - 1) / L][B], const float (&F)[B * (B -
     }
 }
 
+// Pair p of the upper triangle (tri<B> order): its columns
+template <int B>
+struct TriPair {
+    static constexpr int i(int p)
+    {
+        int k = 0;
+        for (int a = 0; a < B; ++a)
+            for (int b = a + 1; b < B; ++b, ++k)
+                if (k == p) return a;
+        return -1;
+    }
+    static constexpr int j(int p)
+    {
+        int k = 0;
+        for (int a = 0; a < B; ++a)
+            for (int b = a + 1; b < B; ++b, ++k)
+                if (k == p) return b;
+        return -1;
+    }
+};
+
+// F_p from the pair's dot product g and the diagonal of G, or 0 if the Jacobi's tests would
+// not rotate the pair (oracle newton_try)
+TMF_DEVI float newton_f(double g, double gi, double gj, double c2)
+{
+    const double g2 = g * g;
+    const bool rot = !(g2 <= c2 * (gi + gj) || g2 <= (JacP<double>::kTol2 * gi) * gj);
+    return rot ? (float)g / (float)(gj - gi) : 0.0f;
+}
+
 // Returns true if the step was taken (same on the L lanes of a block; never when !enable).
+// 2-lane blocks split the pairs: of each couple (p, p+1) in triangle order, lane 0 forms F_p
+// and lane 1 F_(p+1) -- each summing the couple's partial dot products in the butterfly's
+// operand order (p0 + p1 and p1 + p0 are the same bits) -- and the two swap F by one DPP
+// move, so the tests and the IEEE divides run once per pair instead of on both lanes.
 template <int B, int L>
 TMF_DEVI bool newton_try(double (&A)[(B + L - 1) / L][B], double (&V)[(B + L - 1) / L][B], double c2, bool enable)
 {
@@ -1157,22 +1193,43 @@ TMF_DEVI bool newton_try(double (&A)[(B + L - 1) / L][B], double (&V)[(B + L - 1
     static_for<B>([&](auto K) { G[K] = cdot_part<R, B>(A, K, K); });
     static_for<B>([&](auto K) { G[K] = group_sum<L>(G[K]); });
     float F[NP];
-    bool ok = enable;
-    static_for<B>([&](auto I) {
-        constexpr int i = I;
-        static_for<B - 1 - i>([&](auto J0) {
-            constexpr int j = i + 1 + J0, p = tri<B>(i, j);
-            const double g = cdot<R, B, L>(A, i, j), g2 = g * g;
-            const bool rot = !(g2 <= c2 * (G[i] + G[j]) || g2 <= (JacP<double>::kTol2 * G[i]) * G[j]);
-            F[p] = rot ? (float)g / (float)(G[j] - G[i]) : 0.0f;
-            ok = ok && __builtin_fabsf(F[p]) <= kNwtApply;  // NaN / inf fail
+    int ok = enable ? 1 : 0;
+    if constexpr (L == 2) {
+        int q = (int)(__lane_id() & 1);
+        asm volatile("" : "+v"(q));  // a lane mask, not a branch
+        const int m0 = -(int)(q == 0);
+        static_for<NP / 2>([&](auto C) {
+            constexpr int p0 = 2 * C, p1 = p0 + 1;
+            constexpr int i0 = TriPair<B>::i(p0), j0 = TriPair<B>::j(p0), i1 = TriPair<B>::i(p1), j1 = TriPair<B>::j(p1);
+            const double a0 = cdot_part<R, B>(A, i0, j0), a1 = cdot_part<R, B>(A, i1, j1);
+            // lane 0 keeps pair p0 and sends its p1 partial, lane 1 the other way round
+            const double keep = blend(m0, a0, a1), send = blend(m0, a1, a0);
+            const double g = keep + dpp<0xB1>(send);
+            const float f = newton_f(g, blend(m0, G[i0], G[i1]), blend(m0, G[j0], G[j1]), c2);
+            ok &= (int)(__builtin_fabsf(f) <= kNwtApply);  // NaN / inf fail
+            const float other = dpp<0xB1>(f);
+            F[p0] = blend(m0, f, other);
+            F[p1] = blend(m0, other, f);
         });
-    });
-    if (__any(ok)) {
-        apply_f<B, L>(V, F, ok);
-        apply_f<B, L>(A, F, ok);
+        if constexpr (NP % 2 == 1) {  // the last pair on both lanes
+            constexpr int p = NP - 1, i = TriPair<B>::i(p), j = TriPair<B>::j(p);
+            F[p] = newton_f(cdot<R, B, L>(A, i, j), G[i], G[j], c2);
+            ok &= (int)(__builtin_fabsf(F[p]) <= kNwtApply);
+        }
+        ok &= dpp<0xB1>(ok);
+    } else {
+        static_for<NP>([&](auto P) {
+            constexpr int p = P, i = TriPair<B>::i(p), j = TriPair<B>::j(p);
+            F[p] = newton_f(cdot<R, B, L>(A, i, j), G[i], G[j], c2);
+            ok &= (int)(__builtin_fabsf(F[p]) <= kNwtApply);
+        });
     }
-    return ok;
+    const bool take = ok != 0;
+    if (__any(take)) {
+        apply_f<B, L>(V, F, take);
+        apply_f<B, L>(A, F, take);
+    }
+    return take;
 }
 
 // The same step for 4- and 8-lane blocks (b = 10..16), whose B(B-1)/2 F values do not fit

@@ -25,19 +25,24 @@ import csv
 import glob
 import json
 import os
+import re
 
 SIMDS, XCDS = 1024, 8
 CYC = {"plain": 2.0, "f64": 4.0, "trans_f32": 4.0, "trans_f64": 8.0}
 F64 = ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64")
 
 
-def last_dispatch(d, kernel):
-    """counter -> value and (start, end) ns of the last dispatch of `kernel`, over all passes."""
+def last_dispatch(d, kernel, variant=None):
+    """counter -> value and (start, end) ns of the last dispatch of `kernel` (e.g.
+    "embed_kernel<8>"; variant "false" / "true": the strip / list pass instantiation
+    embed_kernel<8, false> / <8, true>), over all passes."""
+    base = re.escape(kernel[:-1])  # "embed_kernel<8"
+    rx = re.compile(base + (r", true>" if variant == "true" else r"(, false)?>"))
     agg, span = {}, {}
     for f in sorted(glob.glob(os.path.join(d, "p*", "**", "*counter_collection.csv"), recursive=True)):
         disp = {}
         for r in csv.DictReader(open(f)):
-            if kernel in r["Kernel_Name"]:
+            if rx.search(r["Kernel_Name"]):
                 k = int(r["Dispatch_Id"])
                 c = disp.setdefault(k, {})
                 c[r["Counter_Name"]] = c.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
@@ -48,6 +53,11 @@ def last_dispatch(d, kernel):
             if "GRBM_GUI_ACTIVE" in disp[k]:
                 agg["_ns"] = span[(f, k)][1] - span[(f, k)][0]
     return agg
+
+
+def add_counters(a, b):
+    """counters of two dispatches (the strip and list passes of one embed call) summed"""
+    return {n: a.get(n, 0.0) + b.get(n, 0.0) for n in set(a) | set(b)}
 
 
 def main():
@@ -76,7 +86,12 @@ def main():
     out.setdefault("kernels", {})
     H, W = a.height, a.width
     for k in ("embed_kernel", "extract_kernel"):
-        c = last_dispatch(a.pmc_dir, f"{k}<{block}>")
+        c = last_dispatch(a.pmc_dir, f"{k}<{block}>", "false" if k == "embed_kernel" else None)
+        lp = last_dispatch(a.pmc_dir, f"{k}<{block}>", "true") if k == "embed_kernel" else {}
+        strip_valu = c["SQ_INSTS_VALU"] / c["SQ_WAVES"]
+        if lp:  # embed's list pass: its work belongs to the same embed call
+            lp_waves, lp_valu = lp.get("SQ_WAVES", 0.0), lp.get("SQ_INSTS_VALU", 0.0)
+            c = add_counters(c, lp)
         waves = c["SQ_WAVES"]
         pw = {n: v / waves for n, v in c.items() if n.startswith("SQ_") and n != "SQ_WAVES"}
         valu = pw["SQ_INSTS_VALU"]
@@ -105,6 +120,10 @@ def main():
             ent["issue_fraction_profiled"] = round(ent["valu_issue_bound_us_per_frame"] / ent["profiled_us_per_frame"], 3)
         if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
             ent["hbm_bytes_per_frame"] = round((2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024 / frames)
+        if lp:
+            ent["strip_pass_valu_instr_per_wave"] = round(strip_valu, 1)
+            ent["list_pass"] = {"waves": lp_waves, "valu_instr": lp_valu,
+                                "note": "counters above are strip + list pass summed (per strip-pass wave count + list waves)"}
         ent["code_id"] = ids.get(f"{k}<{block}>")
         ent["build_id"] = a.build
         out["kernels"][f"{k}<{block}>"] = ent
