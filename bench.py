@@ -154,6 +154,7 @@ def gpu_kernels():
         synth_tile=lambda nbh, nbw, dev: batch.synth_tile(nbh, nbw, device=dev),
         embed=lambda f, t, b, a, o: batch.embed_batch(f, t, b, a, out=o),
         extract=lambda w_, o_, b, a, out: batch.extract_batch(w_, o_, b, a, out=out),
+        embed_stats=lambda f, t, b, a, o: (lambda st: (batch.embed_batch(f, t, b, a, out=o, stats=st), st)[1])({}),
     )
 
 
@@ -359,6 +360,15 @@ def run(args, kernels=None, device=None):
     achieved = embed_bytes / (embed_ms * 1e-3) / 1e9
     achieved_read = F * embed_read / (embed_ms * 1e-3) / 1e9
 
+    # how the embed call's passes split the work, on the batch's first frames (untimed; the same
+    # bytes are rewritten): blocks the strip pass left to the list pass, blocks on the dgesdd route
+    work = None
+    if hasattr(K, "embed_stats") and stop > start:
+        k = min(64, stop - start)
+        st = K.embed_stats(frames[:k], wm, b, alpha, rt.out[:k])
+        work = {"frames": k, "blocks": k * nbh * nbw, "list_pass_blocks": st.get("list_pass_blocks"),
+                "dgesdd_route_blocks": st.get("lapack_blocks")}
+
     # parity of the timed batch against the oracle.  N = 1: rank 0 checks the CPU-baseline
     # sample (the batch's first --cpu-frames frames); N > 1: every rank checks its share of
     # --cpu-frames, spread evenly over its shard.  The first --lapack-frames of the sample
@@ -502,6 +512,8 @@ def run(args, kernels=None, device=None):
             "roofline": {
                 "bound": "hbm",
                 "kernel": f"embed_kernel<{b}>",
+                "launch": f"one tmfwm_embed call: embed_kernel<{b}> strip pass"
+                          + (" + list pass" if b == 8 else "") + f" + embed_fixup_kernel<{b}> (dgesdd route)",
                 "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
@@ -518,6 +530,7 @@ def run(args, kernels=None, device=None):
             "kernels_ms": {"embed": round(embed_ms, 3), "extract": round(extract_ms, 3),
                            "extract_GBs": round(extract_bytes / (extract_ms * 1e-3) / 1e9, 2),
                            "extract_valu_issue": valu.get(f"extract_kernel<{b}>")},
+            "embed_work_sample": work,
             "parity_sample": parity,
             "lapack_route_sample": lapack_sample["summary"] if lapack_sample else None,
             "lapack_route_detail": lapack_sample,

@@ -79,3 +79,21 @@ def test_tolerance_constant_is_glibc_pow():
     src = open(HDR).read()
     m = re.search(r"kTolmul = (0x[0-9a-fp.+-]+);", src)
     assert m and float.fromhex(m.group(1)) == (2.0**-53) ** -0.125
+
+
+def test_workspace_bounds_asan(tmp_path):
+    """The route's workspace indexing stays inside ws_doubles(n) -- the LDS size the fixup
+    kernels give it -- for every n = 1..16 and eight input classes (noise, rank-deficient,
+    zero, tiny / huge scale, ties, a single entry, graded rows), under both host policies:
+    tests/native/lp_asan.cpp under AddressSanitizer, every array its own exact-size heap
+    allocation (the b = 16 fault of the round-2 serial code)."""
+    if not os.path.exists(HIPCC) and not shutil.which("hipcc"):
+        pytest.skip("hipcc not available")
+    exe = tmp_path / "lp_asan"
+    src = os.path.join(ROOT, "tests", "native", "lp_asan.cpp")
+    subprocess.run([HIPCC, "-x", "hip", "--cuda-host-only", "-O1", "-g", "-std=c++17", "-ffp-contract=off",
+                    "-Xarch_host", "-fsanitize=address", "-fno-omit-frame-pointer", src, "-o", str(exe)], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=600,
+                       env=dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=1"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert '"cases": 2048' in r.stdout and '"not_converged": 0' in r.stdout, r.stdout

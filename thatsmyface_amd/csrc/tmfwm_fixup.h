@@ -24,8 +24,13 @@
 
 namespace tmf {
 
-// The block size reaches the dgesdd routines as a run-time value: one instantiation of each
-// (noinline) routine serves every block size of the TU's kernels and the stage entry point.
+// The block size reaches the dgesdd routines as a run-time value, so that the compiler keeps
+// the LAPACK loops as loops instead of unrolling the whole route per block size.  This is not
+// a fault workaround: the workspace indexing stays inside ws_doubles(n) for
+// n = 1..16 under AddressSanitizer (tests/native/lp_asan.cpp, exact-size allocations), and a
+// build with the constant B passes the GPU's dgesdd-route and b = 16 tests
+// (profiles/r03/r03u/constn_tests.log); the round-2 b = 16 fault was in the serial,
+// scratch-array form of the route that round 3 replaced.
 TMF_DEVI int runtime_n(int n)
 {
     asm volatile("" : "+v"(n));
