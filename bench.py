@@ -330,6 +330,15 @@ def run(args, kernels=None, device=None):
 
     for _ in range(args.warmup):
         rt.step()
+    # how one embed call over this rank's whole batch splits its work (untimed; the same bytes
+    # are rewritten, and every embed launch of the run has the same size, so a kernel trace's
+    # averages are the timed launches'): blocks the strip pass left to the list pass, blocks
+    # on the dgesdd route
+    work = None
+    if hasattr(K, "embed_stats") and stop > start:
+        st = K.embed_stats(frames, wm, b, alpha, rt.out)
+        work = {"frames": stop - start, "blocks": (stop - start) * nbh * nbw,
+                "list_pass_blocks": st.get("list_pass_blocks"), "dgesdd_route_blocks": st.get("lapack_blocks")}
     sync()
     if world > 1:
         dist.barrier()
@@ -359,15 +368,6 @@ def run(args, kernels=None, device=None):
     extract_bytes = F * (6 * H * W + nbh * nbw)
     achieved = embed_bytes / (embed_ms * 1e-3) / 1e9
     achieved_read = F * embed_read / (embed_ms * 1e-3) / 1e9
-
-    # how the embed call's passes split the work, on the batch's first frames (untimed; the same
-    # bytes are rewritten): blocks the strip pass left to the list pass, blocks on the dgesdd route
-    work = None
-    if hasattr(K, "embed_stats") and stop > start:
-        k = min(64, stop - start)
-        st = K.embed_stats(frames[:k], wm, b, alpha, rt.out[:k])
-        work = {"frames": k, "blocks": k * nbh * nbw, "list_pass_blocks": st.get("list_pass_blocks"),
-                "dgesdd_route_blocks": st.get("lapack_blocks")}
 
     # parity of the timed batch against the oracle.  N = 1: rank 0 checks the CPU-baseline
     # sample (the batch's first --cpu-frames frames); N > 1: every rank checks its share of

@@ -88,21 +88,32 @@ def main():
     for k in ("embed_kernel", "extract_kernel"):
         c = last_dispatch(a.pmc_dir, f"{k}<{block}>", "false" if k == "embed_kernel" else None)
         lp = last_dispatch(a.pmc_dir, f"{k}<{block}>", "true") if k == "embed_kernel" else {}
-        strip_valu = c["SQ_INSTS_VALU"] / c["SQ_WAVES"]
-        if lp:  # embed's list pass: its work belongs to the same embed call
-            lp_waves, lp_valu = lp.get("SQ_WAVES", 0.0), lp.get("SQ_INSTS_VALU", 0.0)
-            c = add_counters(c, lp)
-        waves = c["SQ_WAVES"]
-        pw = {n: v / waves for n, v in c.items() if n.startswith("SQ_") and n != "SQ_WAVES"}
+
+        def mix(cc):
+            """per-wave instruction classes and spec-rate issue cycles of one dispatch's counters"""
+            w = cc["SQ_WAVES"]
+            pw = {n: v / w for n, v in cc.items() if n.startswith("SQ_") and n != "SQ_WAVES"}
+            f64 = sum(pw.get(n, 0.0) for n in F64)
+            t32, t64 = pw.get("SQ_INSTS_VALU_TRANS_F32", 0.0), pw.get("SQ_INSTS_VALU_TRANS_F64", 0.0)
+            plain = pw["SQ_INSTS_VALU"] - f64 - t32 - t64
+            cyc = plain * CYC["plain"] + f64 * CYC["f64"] + t32 * CYC["trans_f32"] + t64 * CYC["trans_f64"]
+            return pw, f64, t32, t64, cyc
+
+        # per-wave figures: the strip pass (embed) / the kernel (extract); the bound and the time:
+        # every dispatch of the call (embed's list pass, DESIGN.md 4, adds its waves' cycles)
+        pw, f64, t32, t64, cyc = mix(c)
         valu = pw["SQ_INSTS_VALU"]
-        f64 = sum(pw.get(n, 0.0) for n in F64)
-        t32, t64 = pw.get("SQ_INSTS_VALU_TRANS_F32", 0.0), pw.get("SQ_INSTS_VALU_TRANS_F64", 0.0)
-        plain = valu - f64 - t32 - t64
-        cyc = plain * CYC["plain"] + f64 * CYC["f64"] + t32 * CYC["trans_f32"] + t64 * CYC["trans_f64"]
+        waves = c["SQ_WAVES"]
         wpf = waves / frames
-        ns = c.get("_ns")
-        clock = c["GRBM_GUI_ACTIVE"] / XCDS / (ns * 1e-9) if ns else None
-        bound_cyc_frame = cyc * wpf / SIMDS
+        total_cyc = cyc * waves
+        tot = c
+        if lp:
+            lp_cyc = mix(lp)[4]
+            total_cyc += lp_cyc * lp["SQ_WAVES"]
+            tot = add_counters(c, lp)
+        ns = tot.get("_ns")
+        clock = tot["GRBM_GUI_ACTIVE"] / XCDS / (ns * 1e-9) if ns else None
+        bound_cyc_frame = total_cyc / frames / SIMDS
         ent = {
             "frames": frames, "height": H, "width": W,
             "valu_instr_per_wave": round(valu, 1), "f64_arith_per_wave": round(f64, 1),
@@ -118,12 +129,13 @@ def main():
         }
         if ns and clock:
             ent["issue_fraction_profiled"] = round(ent["valu_issue_bound_us_per_frame"] / ent["profiled_us_per_frame"], 3)
-        if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
-            ent["hbm_bytes_per_frame"] = round((2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024 / frames)
+        if "FETCH_SIZE" in tot and "WRITE_SIZE" in tot:
+            ent["hbm_bytes_per_frame"] = round((2 * tot["FETCH_SIZE"] + tot["WRITE_SIZE"]) * 1024 / frames)
         if lp:
-            ent["strip_pass_valu_instr_per_wave"] = round(strip_valu, 1)
-            ent["list_pass"] = {"waves": lp_waves, "valu_instr": lp_valu,
-                                "note": "counters above are strip + list pass summed (per strip-pass wave count + list waves)"}
+            ent["list_pass"] = {"waves": lp["SQ_WAVES"], "valu_instr": lp["SQ_INSTS_VALU"],
+                                "issue_cycles_share": round(1 - cyc * waves / total_cyc, 4),
+                                "note": "per-wave figures are the strip pass's; the bound, the time and the "
+                                        "HBM bytes include the list pass"}
         ent["code_id"] = ids.get(f"{k}<{block}>")
         ent["build_id"] = a.build
         out["kernels"][f"{k}<{block}>"] = ent
