@@ -60,9 +60,10 @@ int tmfwm_abi_version(void);
 const char *tmfwm_last_error(void);
 
 /* Work report of the last tmfwm_embed_ex / tmfwm_extract_ex call on this thread that asked
- * for one (non-NULL n_lapack_blocks): the number of blocks embed's strip pass left to its
- * list pass (blocks needing more f64 Jacobi sweeps than the rest of their wave),
- * 0 for extract; -1 before any such call.  Diagnostics only: the pixels do not depend on it. */
+ * for one (non-NULL n_lapack_blocks): the number of blocks the strip pass left to the list
+ * pass -- embed: blocks needing more f64 Jacobi sweeps than the rest of their wave (DESIGN.md
+ * 4); extract: blocks whose sigma_1 the strip pass's power iterations did not decide (DESIGN.md
+ * 5); -1 before any such call.  Diagnostics only: the output does not depend on it. */
 int64_t tmfwm_last_list_pass_blocks(void);
 
 /* Number of visible HIP devices (0 when none); never fails. */

@@ -766,15 +766,15 @@ static float cdotf(const float *x, const float *y, int ld, int b)
     return tree_sumf(part, P);
 }
 
-/* Phase 1 of the SVD: at most JAC32_MAX_SWEEPS one-sided Jacobi
+/* Phase 1 of the SVD: at most jac32_max_sweeps(b) one-sided Jacobi
  * sweeps in f32 on A32 = D, accumulating V32 (a preconditioner: its V only has to
  * be close to the right singular vectors; phase 3 makes them f64-accurate).
  * Rotate iff gamma^2 > 2^-48 F^2 (gamma above the f32 noise of the whole block),
  * gamma^2 > 2^-45 F (alpha+beta) and gamma^2 > 2^-40 alpha beta.  Blocks with
  * F < 2^-30 skip the phase (V32 = I), which keeps every square in the normal range. */
-#ifndef JAC32_MAX_SWEEPS
-#define JAC32_MAX_SWEEPS 4
-#endif
+/* at most 4 sweeps for b <= 8, 5 from b = 10 on (round 3: with 4, most blocks of the larger
+ * sizes needed a second f64 sweep) */
+static int jac32_max_sweeps(int b) { return b >= 10 ? 5 : 4; }
 #define JAC32_TOL2 9.094947017729282e-13f /* 2^-40 */
 #define JAC32_C2 2.842170943040401e-14f   /* 2^-45 */
 #define JAC32_C2A 3.552713678800501e-15f  /* 2^-48 */
@@ -786,7 +786,7 @@ static int jacobi_f32(float *A, float *V, int b)
     for (int k = 0; k < b; ++k) F += cdotf(A + k, A + k, b, b);
     if (!(F >= JAC32_FMIN)) return 0;
     const float c2 = JAC32_C2 * F, c2a = JAC32_C2A * (F * F);
-    for (sweep = 0; sweep < JAC32_MAX_SWEEPS; ++sweep) {
+    for (sweep = 0; sweep < jac32_max_sweeps(b); ++sweep) {
         int rotated = 0;
         for (int k = 0; k < b; ++k) nrm[k] = cdotf(A + k, A + k, b, b);
         for (int st = 0; st < b - 1; ++st)

@@ -385,8 +385,9 @@ def test_chunked_second_pass_vs_oracle(dev, monkeypatch):
 
 
 def test_list_pass_vs_oracle(dev):
-    """embed's list pass: at b = 8 a wave whose last <= 4 unfinished blocks
-    need another f64 sweep leaves them to the list pass.  Noise covers (1 % of blocks) and
+    """The list passes: at b = 8 an embed wave whose last <= 4 unfinished
+    blocks need another f64 sweep leaves them to the list pass, and extract's undecided sigma_1
+    go to a list pass with more power iterations.  Noise covers (1 % of blocks) and
     camera-like covers (nearly every block needs 2 sweeps, a few 3) both take it; the pixels
     equal the oracle's and a run with the list pass equals itself under chunking."""
     import sys
@@ -404,8 +405,15 @@ def test_list_pass_vs_oracle(dev):
     st = {}
     out = batch.embed_batch(torch.from_numpy(host).to(dev), torch.from_numpy(t).to(dev), b, 0.1, stats=st)
     assert st["list_pass_blocks"] > 0, st
+    refs = [O.embed_frame(host[f], t, b, 0.1) for f in range(len(host))]
     for f in range(len(host)):
-        assert np.array_equal(out[f].cpu().numpy(), O.embed_frame(host[f], t, b, 0.1)), f
+        assert np.array_equal(out[f].cpu().numpy(), refs[f]), f
+    # extract's list pass: blocks 3 power iterations do not certify get 8
+    sx = {}
+    ext = batch.extract_batch(out, torch.from_numpy(host).to(dev), b, 0.1, stats=sx)
+    assert sx["list_pass_blocks"] > 0, sx
+    for f in range(len(host)):
+        assert np.array_equal(ext[f].cpu().numpy(), O.extract_frame(refs[f], host[f], b, 0.1)), f
 
 
 @pytest.mark.parametrize("b", [8, 6, 12, 14])

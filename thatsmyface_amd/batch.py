@@ -88,6 +88,7 @@ def extract_batch(wframes: torch.Tensor, oframes: torch.Tensor, block: int = 8, 
                                       out.data_ptr(), _lib.MEM_DEVICE, _stream(stream), ptr), "extract_batch")
     if stats is not None:
         stats["lapack_blocks"] = int(cnt.value)
+        stats["list_pass_blocks"] = int(L.tmfwm_last_list_pass_blocks())
     return out
 
 

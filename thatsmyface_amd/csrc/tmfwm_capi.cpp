@@ -277,9 +277,10 @@ int run_extract(ExtractArgs a, hipStream_t st, int64_t *n_lapack)
         }
         return 0;
     }
-    DevBuf list, counts;
+    DevBuf list, slow, counts;
     if (int rc = list.alloc((size_t)ch.cap * 4, st, "dgesdd-route block list")) return rc;
-    if (int rc = counts.alloc((size_t)ch.n * 12, st, "block-list counts")) return rc;  // as run_embed's (no list pass)
+    if (int rc = slow.alloc((size_t)ch.cap * 4, st, "list-pass block list")) return rc;
+    if (int rc = counts.alloc((size_t)ch.n * 12, st, "block-list counts")) return rc;  // as run_embed's
     TMF_HIP(hipMemsetAsync(counts.p, 0, (size_t)ch.n * 12, st));
     for (int64_t c = 0; c < ch.n; ++c) {
         ExtractArgs k = a;
@@ -291,6 +292,8 @@ int run_extract(ExtractArgs a, hipStream_t st, int64_t *n_lapack)
         k.fb_list = static_cast<uint32_t *>(list.p);
         k.fb_count = static_cast<uint32_t *>(counts.p) + c;
         k.fb_bad = static_cast<uint32_t *>(counts.p) + ch.n + c;
+        k.slow_list = static_cast<uint32_t *>(slow.p);
+        k.slow_count = static_cast<uint32_t *>(counts.p) + 2 * ch.n + c;
         TMF_HIP(launch_extract(k, st));
         TMF_HIP(launch_extract_fixup(k, k.fb_list, k.fb_count, k.nframes * ch.per_frame, st));
     }

@@ -42,6 +42,10 @@ struct ExtractArgs {
     uint32_t *fb_list;       // blocks whose sigma_1 enclosure is undecided (dgesdd route)
     uint32_t *fb_count;
     uint32_t *fb_bad;        // dgesdd-route blocks whose dbdsqr did not converge (may be null)
+    // list pass: blocks the strip pass's power iterations left undecided, redone
+    // with more iterations before the dgesdd route; null: straight to the dgesdd route
+    uint32_t *slow_list;
+    uint32_t *slow_count;
 };
 
 struct EdgeArgs {

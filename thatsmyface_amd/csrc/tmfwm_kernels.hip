@@ -20,7 +20,11 @@ extern template __global__ void embed_kernel<8, true>(EmbedArgs);
 // ---------------------------------------------------------------------------
 // Extract: watermarking.py:241-289 fused; sigma_1 of both images per block.
 // ---------------------------------------------------------------------------
-constexpr int kPowerIters = 4;    // f32 power iterations before certification
+// f32 power iterations before certification: the strip pass certifies after 3
+// (all but ~0.06 % of noise-cover blocks); the undecided go to the list pass, which certifies
+// after 8, and what it still leaves undecided to the dgesdd route
+constexpr int kPowerIters = 3;
+constexpr int kListPowerIters = 8;
 constexpr int kExtract8Waves = 3;  // waves per SIMD the register allocation of extract<b <= 8> allows
 
 template <int B>
@@ -30,16 +34,11 @@ TMF_DEVI void dct_rows_of(const uint32_t (&words)[Geo<B>::R][Geo<B>::NW], int q,
     dct2d_rows_layout<B, false>(x, tile, q);
 }
 
-template <int B>
-__global__ __launch_bounds__(64, (B > 8 ? 2 : kExtract8Waves)) void extract_kernel(ExtractArgs a)  // waves per SIMD
+// sigma_1 of both images' blocks of this wave (pos per lane), certified or not (ok)
+template <int B, int ITERS>
+TMF_DEVI void extract_sigmas(const ExtractArgs &a, const StripPos &pos, float *tile, int q, float &sw, float &so, bool &ok)
 {
-    constexpr int L = Geo<B>::L, R = Geo<B>::R, BPW = Geo<B>::BPW, LD = B + 1;
-    __shared__ float lds[BPW * B * LD];
-    const int lane = threadIdx.x & 63, g = lane / L, q = lane % L;
-    float *tile = lds + g * B * LD;
-    const StripPos pos = strip_pos<B>(a.strips_per_row, a.nbw);
-    float sw, so;
-    bool ok;
+    constexpr int R = Geo<B>::R, L = Geo<B>::L;
     if constexpr (B <= 12) {
         // both images' rows requested up front (one exposed HBM latency per wave, not two),
         // and both power iterations interleaved (sigma1_certified, NI = 2)
@@ -53,7 +52,7 @@ __global__ __launch_bounds__(64, (B > 8 ? 2 : kExtract8Waves)) void extract_kern
         }
         float s[2];
         bool k[2];
-        sigma1_certified<B, L, kPowerIters, 2>(x, s, k);
+        sigma1_certified<B, L, ITERS, 2>(x, s, k);
         sw = s[0];
         so = s[1];
         ok = k[0] && k[1];
@@ -63,27 +62,68 @@ __global__ __launch_bounds__(64, (B > 8 ? 2 : kExtract8Waves)) void extract_kern
         bool k[1];
         load_block_rows<B>(a.wsrc + pos.frame * a.frame_stride, a.W, pos, q, a.aligned, w);
         dct_rows_of<B>(w, q, tile, x[0]);
-        sigma1_certified<B, L, kPowerIters, 1>(x, s, k);
+        sigma1_certified<B, L, ITERS, 1>(x, s, k);
         sw = s[0];
         ok = k[0];
         load_block_rows<B>(a.osrc + pos.frame * a.frame_stride, a.W, pos, q, a.aligned, w);
         dct_rows_of<B>(w, q, tile, x[0]);
-        sigma1_certified<B, L, kPowerIters, 1>(x, s, k);
+        sigma1_certified<B, L, ITERS, 1>(x, s, k);
         so = s[0];
         ok = ok && k[0];
     }
-    if (!pos.valid || q != 0) return;
-    const uint32_t id = (uint32_t)(((int64_t)blockIdx.y * a.nbh + pos.bi) * a.nbw + pos.bj);
-    if (!ok) {  // the enclosure did not decide f32(sigma_1): dgesdd route (extract_fixup_kernel)
-        a.fb_list[atomicAdd(a.fb_count, 1u)] = id;
-        return;
-    }
-    // :285 under numpy-2 NEP 50: (f32 - f32) / f32(alpha) in f32; :288-289 clip, *255 in f64, trunc
-    const float e = (sw - so) / a.alpha32;
+}
+
+// :285 under numpy-2 NEP 50: (f32 - f32) / f32(alpha) in f32; :288-289 clip, *255 in f64, trunc
+TMF_DEVI uint8_t extract_byte(float sw, float so, float alpha32)
+{
+    const float e = (sw - so) / alpha32;
     double d = (double)e;
     d = d < 0.0 ? 0.0 : d;
     d = d > 1.0 ? 1.0 : d;
-    a.out[pos.frame * a.tile_stride + (int64_t)pos.bi * a.nbw + pos.bj] = (uint8_t)(uint32_t)(d * 255.0);
+    return (uint8_t)(uint32_t)(d * 255.0);
+}
+
+template <int B, bool LIST = false>
+__global__ __launch_bounds__(64, (B > 8 ? 2 : kExtract8Waves)) void extract_kernel(ExtractArgs a)  // waves per SIMD
+{
+    constexpr int L = Geo<B>::L, BPW = Geo<B>::BPW, LD = B + 1;
+    __shared__ float lds[BPW * B * LD];
+    const int lane = threadIdx.x & 63, g = lane / L, q = lane % L;
+    float *tile = lds + g * B * LD;
+    if constexpr (LIST) {
+        // grid-stride over the list of blocks the strip pass left undecided
+        const uint32_t n = *a.slow_count, per_frame = (uint32_t)a.nbh * (uint32_t)a.nbw;
+        for (uint32_t t0 = blockIdx.x * BPW; t0 < n; t0 += gridDim.x * BPW) {
+            StripPos pos;
+            pos.valid = t0 + g < n;
+            const uint32_t id = pos.valid ? a.slow_list[t0 + g] : 0u;
+            pos.frame = id / per_frame;
+            const uint32_t rem = id % per_frame;
+            pos.bi = (int)(rem / (uint32_t)a.nbw);
+            pos.bj = (int)(rem % (uint32_t)a.nbw);
+            float sw, so;
+            bool ok;
+            extract_sigmas<B, kListPowerIters>(a, pos, tile, q, sw, so, ok);
+            if (pos.valid && q == 0) {
+                if (ok) a.out[pos.frame * a.tile_stride + (int64_t)pos.bi * a.nbw + pos.bj] = extract_byte(sw, so, a.alpha32);
+                else a.fb_list[atomicAdd(a.fb_count, 1u)] = id;  // dgesdd route (extract_fixup_kernel)
+            }
+            __syncthreads();  // the LDS tiles are reused by the next listed blocks
+        }
+    } else {
+        const StripPos pos = strip_pos<B>(a.strips_per_row, a.nbw);
+        float sw, so;
+        bool ok;
+        extract_sigmas<B, kPowerIters>(a, pos, tile, q, sw, so, ok);
+        if (!pos.valid || q != 0) return;
+        const uint32_t id = (uint32_t)(((int64_t)blockIdx.y * a.nbh + pos.bi) * a.nbw + pos.bj);
+        if (!ok) {  // the enclosure did not decide f32(sigma_1): list pass, or the dgesdd route
+            if (a.slow_list) a.slow_list[atomicAdd(a.slow_count, 1u)] = id;
+            else a.fb_list[atomicAdd(a.fb_count, 1u)] = id;
+            return;
+        }
+        a.out[pos.frame * a.tile_stride + (int64_t)pos.bi * a.nbw + pos.bj] = extract_byte(sw, so, a.alpha32);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -298,7 +338,19 @@ static hipError_t launch_embed_b(EmbedArgs a, hipStream_t st)
     return hipGetLastError();
 }
 
-bool embed_defers(int block) { return block == 8 ? kDeferMax<8> > 0 : false; }
+bool embed_defers(int block)
+{
+    switch (block) {
+    case 4: return kDeferMax<4> > 0;
+    case 6: return kDeferMax<6> > 0;
+    case 8: return kDeferMax<8> > 0;
+    case 10: return kDeferMax<10> > 0;
+    case 12: return kDeferMax<12> > 0;
+    case 14: return kDeferMax<14> > 0;
+    case 16: return kDeferMax<16> > 0;
+    default: return false;
+    }
+}
 
 hipError_t launch_embed(const EmbedArgs &a, hipStream_t st)
 {
@@ -353,7 +405,12 @@ static hipError_t launch_extract_b(ExtractArgs a, hipStream_t st)
         c.wsrc = a.wsrc + f0 * a.frame_stride;
         c.osrc = a.osrc + f0 * a.frame_stride;
         c.out = a.out + f0 * a.tile_stride;
-        hipLaunchKernelGGL(extract_kernel<B>, dim3((unsigned)gx, (unsigned)nf), dim3(64), 0, st, c);
+        hipLaunchKernelGGL((extract_kernel<B, false>), dim3((unsigned)gx, (unsigned)nf), dim3(64), 0, st, c);
+    }
+    if (a.slow_list) {  // the list pass over the undecided blocks (ids relative to a.wsrc / a.osrc)
+        const int64_t waves = ((int64_t)a.nframes * a.nbh * a.nbw + Geo<B>::BPW - 1) / Geo<B>::BPW;
+        const unsigned grid = (unsigned)(waves < kListPassGrid ? waves : kListPassGrid);
+        hipLaunchKernelGGL((extract_kernel<B, true>), dim3(grid), dim3(64), 0, st, a);
     }
     return hipGetLastError();
 }
