@@ -772,9 +772,10 @@ static float cdotf(const float *x, const float *y, int ld, int b)
  * Rotate iff gamma^2 > 2^-48 F^2 (gamma above the f32 noise of the whole block),
  * gamma^2 > 2^-45 F (alpha+beta) and gamma^2 > 2^-40 alpha beta.  Blocks with
  * F < 2^-30 skip the phase (V32 = I), which keeps every square in the normal range. */
-/* at most 4 sweeps for b <= 8, 5 from b = 10 on (round 3: with 4, most blocks of the larger
- * sizes needed a second f64 sweep) */
-static int jac32_max_sweeps(int b) { return b >= 10 ? 5 : 4; }
+#ifndef JAC32_MAX_SWEEPS
+#define JAC32_MAX_SWEEPS 4
+#endif
+static int jac32_max_sweeps(int b) { (void)b; return JAC32_MAX_SWEEPS; }
 #define JAC32_TOL2 9.094947017729282e-13f /* 2^-40 */
 #define JAC32_C2 2.842170943040401e-14f   /* 2^-45 */
 #define JAC32_C2A 3.552713678800501e-15f  /* 2^-48 */

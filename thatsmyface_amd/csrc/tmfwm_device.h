@@ -686,11 +686,10 @@ template <> struct JacP<double> {
 };
 template <> struct JacP<float> {
     static constexpr bool kBranchy = false;
-    // sweeps of phase 1 (oracle jac32_max_sweeps): 5 from b = 10 on, where 4 leave most
-    // blocks a second f64 sweep (b = 16 noise covers: 91 % -> 14 % of the blocks, embed<10>
-    // / <12> -9 %, <14> -6 %, <16> -2 %; profiles/r03/r03x/), 4 below (b = 8: 99 % finish in
-    // one f64 sweep already, a fifth f32 sweep would cost ~9 %)
-    static constexpr int max_sweeps(int b) { return b >= 10 ? 5 : 4; }
+    // sweeps of phase 1 (oracle JAC32_MAX_SWEEPS).  5 from b = 10 on was measured in round 3:
+    // embed<10> / <12> -9 %, <14> -7 %, <16> -3 % on noise covers, but +4..5 % on camera-like
+    // covers (profiles/r03/r03y/, r03z/), so every size keeps 4
+    static constexpr int max_sweeps(int) { return 4; }
     static constexpr float kTol2 = 9.094947017729282e-13f;  // 2^-40
     static constexpr float kC2 = 2.842170943040401e-14f;    // 2^-45
     static constexpr float kC2A = 3.552713678800501e-15f;   // 2^-48

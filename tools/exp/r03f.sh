@@ -1,0 +1,7 @@
+# final round-3 pass on the shipped build: GPU suite, then tools/profile_round.sh (bench line,
+# rocprofv3 kernel trace of the same command, counter passes at b = 8 / 16, phase stamps)
+set -euo pipefail
+TAG=${TAG:-r03f}
+mkdir -p gpurun_out/$TAG
+timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/$TAG/gpu_tests.log 2>&1
+bash tools/profile_round.sh $TAG
