@@ -967,6 +967,14 @@ TMF_DEVI int jacobi_sweep(T (&A)[(B + L - 1) / L][B], T (&V)[(B + L - 1) / L][B]
     T *prm = nl + (kLN ? 16 : 0);
     constexpr bool kLS = kLdsSums<L, T> && PP == 1;
     T *part = nl + 32;  // kLS: partial of pair p from lane k at part[p * 8 + k]
+    if constexpr (kLN && B == 16) {
+        // q through an opaque move (as in newton_try_lds): the per-round pair columns derived
+        // from it are otherwise hoisted out of the sweep loop, held across it and spilled --
+        // 4 scratch reloads per round at b = 16 (spilled VGPRs 74 -> 47, none left inside the
+        // f64 loop; embed<16> -2.4 % noise / -1.6 % camera-like covers, profiles/r03/r03i/;
+        // b = 14 has no spill to remove and measured +1 %)
+        asm volatile("" : "+v"(q));
+    }
     T nrm[B];
     // batches of dot products: all lane-local chains first, then all cross-lane sums,
     // so that the chains interleave and no DPP read waits on the write just before it
