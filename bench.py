@@ -155,6 +155,7 @@ def gpu_kernels():
         embed=lambda f, t, b, a, o: batch.embed_batch(f, t, b, a, out=o),
         extract=lambda w_, o_, b, a, out: batch.extract_batch(w_, o_, b, a, out=out),
         embed_stats=lambda f, t, b, a, o: (lambda st: (batch.embed_batch(f, t, b, a, out=o, stats=st), st)[1])({}),
+        embed_list_pass=batch.embed_list_pass,
     )
 
 
@@ -359,6 +360,11 @@ def run(args, kernels=None, device=None):
     else:
         embed_ms = sum(m - a for a, m, _ in ev) / len(ev) * 1e3
         extract_ms = sum(z - m for _, m, z in ev) / len(ev) * 1e3
+    # every rank's mean launch times (the line's roofline is rank 0's; N > 1 adds the spread)
+    launch_ranks = [(embed_ms, extract_ms)]
+    if world > 1:
+        launch_ranks = [None] * world
+        dist.all_gather_object(launch_ranks, (embed_ms, extract_ms))
     px_step = F * H * W * world
     value = px_step * args.steps / elapsed / 1e6
 
@@ -377,11 +383,13 @@ def run(args, kernels=None, device=None):
     # conditioning flag, which the default (hybrid) route shares with the GPU.
     cpu, parity = None, None
     n_local = stop - start
-    want_cpu = rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_frames > 0
+    # N = 1: rank 0 times the sample on all host cores; N > 1: every rank checks its share at
+    # the same time on cores / world, and rank 0's share is the reported baseline
+    want_cpu = rank == 0 and not args.no_cpu_baseline and args.cpu_frames > 0 and n_local > 0
     checked = bad_e = bad_x = 0
     lp_checked = lp_bad_e = lp_bad_x = 0
-    if want_cpu or (world > 1 and n_local > 0 and args.cpu_frames > 0):
-        if want_cpu:
+    if (want_cpu and world == 1) or (world > 1 and n_local > 0 and args.cpu_frames > 0):
+        if world == 1:
             idx = list(range(min(args.cpu_frames, n_local)))
         else:
             k = min(n_local, max(1, -(-args.cpu_frames // world)))
@@ -395,12 +403,14 @@ def run(args, kernels=None, device=None):
         n_lp = min(checked, args.lapack_frames if world == 1 else -(-args.lapack_frames // world))
         lp_checked, lp_bad_e, lp_bad_x = lapack_check(host[:n_lp], host_tile, gout[:n_lp], gtiles[:n_lp], b, alpha, threads)
         if want_cpu:
+            which = (f"the batch's first {checked}" if world == 1 else
+                     f"rank 0's share of the parity sample, checked while the other {world - 1} ranks check theirs")
             cpu = {
                 "value": round(checked * H * W / dt / 1e6, 3),
                 "unit": "Mpixels/s",
                 "cores": threads,
                 "kind": "port",
-                "sample": f"{checked} synthetic {W}x{H} frames (the batch's first {checked}), embed+extract round trip, "
+                "sample": f"{checked} synthetic {W}x{H} frames ({which}), embed+extract round trip, "
                           f"oracle/tmfwm_oracle.c with {threads} OpenMP threads, {dt:.2f} s",
             }
     if world > 1:  # every rank joins, checked or not
@@ -424,7 +434,7 @@ def run(args, kernels=None, device=None):
     # compared with the same region of the GPU's output (equal where this host's OpenBLAS
     # core is the reference's SkylakeX)
     structured = None
-    if want_cpu and args.structured_crops > 0:
+    if want_cpu and world == 1 and args.structured_crops > 0:
         from oracle import structured as ST
 
         ch, cw = min(H, 68 * b), min(W, 120 * b)
@@ -450,9 +460,10 @@ def run(args, kernels=None, device=None):
     build = lib_build_id() if on_gpu else None
 
     # Counter-derived figures (tools/pmc_embed.sh -> tools/valu.py -> profiles/valu.json) are
-    # used only for the device code they measured: each entry carries the code id of its
-    # kernel's TU (tools/kernel_ids.py -> libtmfwm.kernels.json, written when the library is
-    # linked), so a rebuild that leaves the kernel's code unchanged keeps its profile.
+    # used only for the device code they measured: each entry carries its kernel's code id (a
+    # hash of the kernel's own machine code and descriptors, tools/kernel_ids.py ->
+    # libtmfwm.kernels.json, written when the library is linked), so a rebuild that leaves the
+    # kernel's code unchanged keeps its profile.
     ids = kernel_code_ids() if on_gpu else {}
     vj = _profile_json("valu.json")
 
@@ -513,7 +524,8 @@ def run(args, kernels=None, device=None):
                 "bound": "hbm",
                 "kernel": f"embed_kernel<{b}>",
                 "launch": f"one tmfwm_embed call: embed_kernel<{b}> strip pass"
-                          + (" + list pass" if b == 8 else "") + f" + embed_fixup_kernel<{b}> (dgesdd route)",
+                          + (" + list pass" if getattr(K, "embed_list_pass", lambda _b: False)(b) else "")
+                          + f" + embed_fixup_kernel<{b}> (dgesdd route)",
                 "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
@@ -523,11 +535,15 @@ def run(args, kernels=None, device=None):
                 "read_frac": round(achieved_read / HBM_PEAK_GBS, 5),
                 "algorithmic_bytes_per_launch": embed_bytes,
                 "launch_ms": round(embed_ms, 3),
+                "launch_ms_over_ranks": {"max": round(max(e for e, _ in launch_ranks), 3),
+                                         "min": round(min(e for e, _ in launch_ranks), 3), "ranks": world},
                 "copy_peak_measured_GBs": copy_gbs,
                 "binding_bound": "VALU issue (DESIGN.md section 4), not HBM",
                 "valu_issue": valu.get(f"embed_kernel<{b}>"),
             },
             "kernels_ms": {"embed": round(embed_ms, 3), "extract": round(extract_ms, 3),
+                           "extract_over_ranks": {"max": round(max(x for _, x in launch_ranks), 3),
+                                                  "min": round(min(x for _, x in launch_ranks), 3)},
                            "extract_GBs": round(extract_bytes / (extract_ms * 1e-3) / 1e9, 2),
                            "extract_valu_issue": valu.get(f"extract_kernel<{b}>")},
             "embed_work_sample": work,

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define TMFWM_ABI_VERSION 6
+#define TMFWM_ABI_VERSION 7
 
 #define TMFWM_MEM_HOST 0
 #define TMFWM_MEM_DEVICE 1
@@ -66,6 +66,12 @@ const char *tmfwm_last_error(void);
  * 5); -1 before any such call.  Diagnostics only: the output does not depend on it. */
 int64_t tmfwm_last_list_pass_blocks(void);
 
+/* 1 when tmfwm_embed at this block size runs a list pass after its strip pass (the strip pass
+ * may leave blocks that need more f64 Jacobi sweeps than the rest of their wave to it,
+ * DESIGN.md 4), else 0 (also for unsupported sizes).  Describes the launches of a call; the
+ * output does not depend on it.  (ABI 7) */
+int tmfwm_embed_list_pass(int32_t block);
+
 /* Number of visible HIP devices (0 when none); never fails. */
 int tmfwm_device_count(void);
 
@@ -84,6 +90,11 @@ int tmfwm_embed(const uint8_t *rgb, int64_t n_frames, int32_t height, int32_t wi
  * number of blocks that took the dgesdd route.  Passing it makes the call wait for
  * `hip_stream` (the count lives on the device); NULL keeps TMFWM_MEM_DEVICE calls
  * asynchronous.
+ *
+ * A dgesdd-route block on which dbdsqr does not converge (np.linalg.svd raises LinAlgError
+ * there) fails the call with TMFWM_ERR_HIP whenever the call synchronises: every
+ * TMFWM_MEM_HOST call, and every call with a non-NULL n_lapack_blocks.  An asynchronous
+ * TMFWM_MEM_DEVICE call without a count pointer cannot report it (the same holds for extract).
  */
 int tmfwm_embed_ex(const uint8_t *rgb, int64_t n_frames, int32_t height, int32_t width, int64_t frame_stride,
                    const uint8_t *wm_tile, int32_t block, double alpha, uint8_t *out, int32_t mem_kind, void *hip_stream,

@@ -646,6 +646,34 @@ def test_overlapping_buffers_refused(dev):
                                    _lib.MEM_DEVICE, st), "extract")
 
 
+def test_nonconvergence_reported_by_synchronising_calls(dev, monkeypatch):
+    """A dgesdd-route block whose dbdsqr does not converge (np.linalg.svd raises LinAlgError) fails
+    every call that synchronises -- the host-memory drop-in path and the _ex calls -- even when
+    the caller asked for no count; TMFWM_DEBUG_FORCE_NONCONV marks one block per
+    chunk.  The asynchronous device call without a count pointer cannot see it (tmfwm.h)."""
+    from thatsmyface_amd import _lib, batch
+    from thatsmyface_amd import watermarking as W
+
+    b, h, w = 8, 64, 96
+    rgb = _u8(7, (h, w, 3))
+    wm = _u8(8, (13, 17))
+    s = {"block_size": b, "alpha": 0.1}
+    e = W.embed_watermark(Image.fromarray(rgb), Image.fromarray(wm, "L"), False, s)  # sane without the flag
+    monkeypatch.setenv("TMFWM_DEBUG_FORCE_NONCONV", "1")
+    with pytest.raises(RuntimeError, match="did not converge"):
+        W.embed_watermark(Image.fromarray(rgb), Image.fromarray(wm, "L"), False, s)
+    with pytest.raises(RuntimeError, match="did not converge"):
+        W.extract_watermark(e, Image.fromarray(rgb), s)
+    fr = torch.from_numpy(rgb[None].copy()).to(dev)
+    tile = torch.from_numpy(_u8(9, (h // b, w // b))).to(dev)
+    with pytest.raises(RuntimeError, match="did not converge"):
+        batch.embed_batch(fr, tile, b, 0.1, stats={})
+    batch.embed_batch(fr, tile, b, 0.1)  # async, no count pointer: not checked
+    torch.cuda.synchronize()
+    L = _lib.load()
+    assert [L.tmfwm_embed_list_pass(k) for k in (4, 6, 8, 10, 12, 14, 16, 7, 18)] == [0, 0, 1, 0, 0, 0, 0, 0, 0]
+
+
 def test_multi_entry_points_logical_shards(dev, monkeypatch):
     """tmfwm_embed_multi / tmfwm_extract_multi (host memory, one thread + stream per shard):
     three logical shards on device 0 == one device-resident batch == the oracle; with

@@ -14,7 +14,7 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # TMFWM_LIB selects an alternative build (e.g. the phase-profile libtmfwm_stamps.so)
 LIB_PATH = os.environ.get("TMFWM_LIB") or os.path.join(_HERE, "libtmfwm.so")
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 MEM_HOST = 0
 MEM_DEVICE = 1
@@ -44,6 +44,7 @@ SIGNATURES = {
     "tmfwm_embed": (ctypes.c_int, [_VP, _I64, _I32, _I32, _I64, _VP, _I32, _D, _VP, _I32, _VP]),
     "tmfwm_extract": (ctypes.c_int, [_VP, _VP, _I64, _I32, _I32, _I64, _I32, _D, _VP, _I32, _VP]),
     "tmfwm_last_list_pass_blocks": (ctypes.c_int64, []),
+    "tmfwm_embed_list_pass": (ctypes.c_int, [ctypes.c_int32]),
     "tmfwm_embed_ex": (ctypes.c_int, [_VP, _I64, _I32, _I32, _I64, _VP, _I32, _D, _VP, _I32, _VP, _VP]),
     "tmfwm_extract_ex": (ctypes.c_int, [_VP, _VP, _I64, _I32, _I32, _I64, _I32, _D, _VP, _I32, _VP, _VP]),
     "tmfwm_embed_multi": (ctypes.c_int, [_VP, _I64, _I32, _I32, _I64, _VP, _I32, _D, _VP, _VP, _I32, _VP]),

@@ -39,6 +39,11 @@ def _count_ptr(stats):
     return c, ctypes.addressof(c)
 
 
+def embed_list_pass(block: int) -> bool:
+    """Whether embed at this block size runs a list pass after its strip pass."""
+    return bool(_lib.load().tmfwm_embed_list_pass(int(block)))
+
+
 def embed_batch(frames: torch.Tensor, wm_tile: torch.Tensor, block: int = 8, alpha: float = 0.1,
                 out: torch.Tensor | None = None, stream=None, stats: dict | None = None) -> torch.Tensor:
     """Embed one watermark tile into every frame (watermarking.py:135 per frame).

@@ -162,6 +162,14 @@ size_t span_bytes(int64_t n, int64_t stride, int64_t frame_bytes) { return n == 
 // TMFWM_DEBUG_LIST_CAP (ids) lowers it so that the tests can exercise several chunks.
 constexpr int64_t kListCap = int64_t(1) << 29;
 
+// TMFWM_DEBUG_FORCE_NONCONV=1 marks one dgesdd-route block of every chunk as not converged
+// (tests: the non-convergence report of the synchronising calls, include/tmfwm.h)
+bool force_nonconv()
+{
+    const char *e = std::getenv("TMFWM_DEBUG_FORCE_NONCONV");
+    return e && *e && *e != '0';
+}
+
 int64_t list_cap()
 {
     const char *e = std::getenv("TMFWM_DEBUG_LIST_CAP");
@@ -192,7 +200,10 @@ int sum_counts(const uint32_t *dcounts, int64_t nchunks, hipStream_t st, int64_t
     if (nchunks) {
         hipError_t e = hipMemcpyAsync(h.data(), dcounts, (size_t)nchunks * 12, hipMemcpyDeviceToHost, st);
         if (e == hipSuccess) e = hipStreamSynchronize(st);
-        if (e != hipSuccess) return fail(TMFWM_ERR_HIP, "reading the dgesdd-route counts failed: %s", hipGetErrorString(e));
+        if (e != hipSuccess) {
+            t_list_pass = -1;
+            return fail(TMFWM_ERR_HIP, "reading the dgesdd-route counts failed: %s", hipGetErrorString(e));
+        }
     }
     int64_t t = 0, bad = 0, slow = 0;
     for (int64_t c = 0; c < nchunks; ++c) {
@@ -200,7 +211,7 @@ int sum_counts(const uint32_t *dcounts, int64_t nchunks, hipStream_t st, int64_t
         bad += h[(size_t)(nchunks + c)];
         slow += h[(size_t)(2 * nchunks + c)];
     }
-    *out = t;
+    if (out) *out = t;
     t_list_pass = slow;
     if (bad)
         return fail(TMFWM_ERR_HIP, "dgesdd route: dbdsqr did not converge on %lld block(s) (np.linalg.svd raises LinAlgError there)",
@@ -226,8 +237,13 @@ void clear_error() { t_err.clear(); }
 
 int check_frames(int64_t n, int32_t H, int32_t W, int64_t stride, int32_t block) { return ::check_frames(n, H, W, stride, block); }
 
-// Both passes of embed over device-resident frames (a.src / a.dst / a.wm set).
-int run_embed(EmbedArgs a, hipStream_t st, int64_t *n_lapack)
+// Both passes of embed over device-resident frames (a.src / a.dst / a.wm set).  The
+// per-chunk counts (dgesdd-route blocks, dbdsqr non-convergence, list-pass blocks) are read
+// back -- which synchronises the stream -- when the caller asks for the count (n_lapack) or
+// when `check` is set (the host-memory calls, which synchronise anyway): a dbdsqr that did not
+// converge then fails the call (np.linalg.svd raises LinAlgError there).  An asynchronous
+// device-memory call without a count pointer is not checked (include/tmfwm.h).
+int run_embed(EmbedArgs a, hipStream_t st, int64_t *n_lapack, bool check)
 {
     Chunks ch;
     ch.plan(a.nframes, (int64_t)a.nbh * a.nbw);
@@ -261,12 +277,13 @@ int run_embed(EmbedArgs a, hipStream_t st, int64_t *n_lapack)
         k.slow_count = static_cast<uint32_t *>(counts.p) + 2 * ch.n + c;
         TMF_HIP(launch_embed(k, st));
         TMF_HIP(launch_embed_fixup(k, k.fb_list, k.fb_count, k.nframes * ch.per_frame, st));
+        if (force_nonconv()) TMF_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(k.fb_bad), 1, 1, st));
     }
-    if (n_lapack) return sum_counts(static_cast<const uint32_t *>(counts.p), ch.n, st, n_lapack);
+    if (n_lapack || check) return sum_counts(static_cast<const uint32_t *>(counts.p), ch.n, st, n_lapack);
     return 0;
 }
 
-int run_extract(ExtractArgs a, hipStream_t st, int64_t *n_lapack)
+int run_extract(ExtractArgs a, hipStream_t st, int64_t *n_lapack, bool check)
 {
     Chunks ch;
     ch.plan(a.nframes, (int64_t)a.nbh * a.nbw);
@@ -296,8 +313,9 @@ int run_extract(ExtractArgs a, hipStream_t st, int64_t *n_lapack)
         k.slow_count = static_cast<uint32_t *>(counts.p) + 2 * ch.n + c;
         TMF_HIP(launch_extract(k, st));
         TMF_HIP(launch_extract_fixup(k, k.fb_list, k.fb_count, k.nframes * ch.per_frame, st));
+        if (force_nonconv()) TMF_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(k.fb_bad), 1, 1, st));
     }
-    if (n_lapack) return sum_counts(static_cast<const uint32_t *>(counts.p), ch.n, st, n_lapack);
+    if (n_lapack || check) return sum_counts(static_cast<const uint32_t *>(counts.p), ch.n, st, n_lapack);
     return 0;
 }
 }  // namespace tmf
@@ -309,6 +327,8 @@ int tmfwm_abi_version(void) { return TMFWM_ABI_VERSION; }
 const char *tmfwm_last_error(void) { return t_err.c_str(); }
 
 int64_t tmfwm_last_list_pass_blocks(void) { return t_list_pass; }
+
+int tmfwm_embed_list_pass(int32_t block) { return supported_block(block) && tmf::embed_defers(block) ? 1 : 0; }
 
 int tmfwm_device_count(void)
 {
@@ -325,7 +345,10 @@ int tmfwm_embed_ex(const uint8_t *rgb, int64_t n_frames, int32_t height, int32_t
                    int64_t *n_lapack_blocks)
 {
     t_err.clear();
-    if (n_lapack_blocks) *n_lapack_blocks = 0;
+    if (n_lapack_blocks) {
+        *n_lapack_blocks = 0;
+        t_list_pass = 0;  // this call's count from here on (an early return leaves 0)
+    }
     if (int rc = check_frames(n_frames, height, width, frame_stride, block)) return rc;
     if (!std::isfinite(alpha)) return fail(TMFWM_ERR_INVALID, "alpha is not finite");
     if (int rc = need_device()) return rc;
@@ -355,7 +378,7 @@ int tmfwm_embed_ex(const uint8_t *rgb, int64_t n_frames, int32_t height, int32_t
         a.dst = out;
         a.wm = wm_tile;
         a.aligned = ((reinterpret_cast<uintptr_t>(rgb) | reinterpret_cast<uintptr_t>(out)) % 4 == 0) && frame_stride % 4 == 0 && width % 4 == 0;
-        return tmf::run_embed(a, st, n_lapack_blocks);
+        return tmf::run_embed(a, st, n_lapack_blocks, false);
     }
     if (mem_kind != TMFWM_MEM_HOST) return fail(TMFWM_ERR_INVALID, "mem_kind %d", mem_kind);
     if (!rgb || !out || (tbytes && !wm_tile)) return fail(TMFWM_ERR_INVALID, "NULL host pointer");
@@ -369,7 +392,7 @@ int tmfwm_embed_ex(const uint8_t *rgb, int64_t n_frames, int32_t height, int32_t
     a.dst = static_cast<uint8_t *>(dout.p);
     a.wm = static_cast<const uint8_t *>(dwm.p);
     a.aligned = frame_stride % 4 == 0 && width % 4 == 0;
-    if (int rc = tmf::run_embed(a, st, n_lapack_blocks)) return rc;
+    if (int rc = tmf::run_embed(a, st, n_lapack_blocks, true)) return rc;
     if (frame_stride == fbytes) {
         TMF_HIP(hipMemcpyAsync(out, dout.p, span, hipMemcpyDeviceToHost, st));
     } else {
@@ -392,7 +415,10 @@ int tmfwm_extract_ex(const uint8_t *wm_rgb, const uint8_t *orig_rgb, int64_t n_f
                      int64_t *n_lapack_blocks)
 {
     t_err.clear();
-    if (n_lapack_blocks) *n_lapack_blocks = 0;
+    if (n_lapack_blocks) {
+        *n_lapack_blocks = 0;
+        t_list_pass = 0;  // this call's count from here on (an early return leaves 0)
+    }
     if (int rc = check_frames(n_frames, height, width, frame_stride, block)) return rc;
     if (!std::isfinite(alpha) || alpha == 0.0) return fail(TMFWM_ERR_INVALID, "alpha must be finite and non-zero");
     if (int rc = need_device()) return rc;
@@ -423,7 +449,7 @@ int tmfwm_extract_ex(const uint8_t *wm_rgb, const uint8_t *orig_rgb, int64_t n_f
         a.osrc = orig_rgb;
         a.out = out_tiles;
         a.aligned = ((reinterpret_cast<uintptr_t>(wm_rgb) | reinterpret_cast<uintptr_t>(orig_rgb)) % 4 == 0) && frame_stride % 4 == 0 && width % 4 == 0;
-        return tmf::run_extract(a, st, n_lapack_blocks);
+        return tmf::run_extract(a, st, n_lapack_blocks, false);
     }
     if (mem_kind != TMFWM_MEM_HOST) return fail(TMFWM_ERR_INVALID, "mem_kind %d", mem_kind);
     if (!wm_rgb || !orig_rgb || !out_tiles) return fail(TMFWM_ERR_INVALID, "NULL host pointer");
@@ -437,7 +463,7 @@ int tmfwm_extract_ex(const uint8_t *wm_rgb, const uint8_t *orig_rgb, int64_t n_f
     a.osrc = static_cast<const uint8_t *>(dor.p);
     a.out = static_cast<uint8_t *>(dout.p);
     a.aligned = frame_stride % 4 == 0 && width % 4 == 0;
-    if (int rc = tmf::run_extract(a, st, n_lapack_blocks)) return rc;
+    if (int rc = tmf::run_extract(a, st, n_lapack_blocks, true)) return rc;
     TMF_HIP(hipMemcpyAsync(out_tiles, dout.p, (size_t)(tbytes * n_frames), hipMemcpyDeviceToHost, st));
     TMF_HIP(hipStreamSynchronize(st));
     return 0;

@@ -98,8 +98,12 @@ def ycbcr_to_rgb(img) -> np.ndarray:
     """watermarking.py:53-73 on the GPU: (H, W, 3) float16/32/64 -> (H, W, 3) uint8, in
     the input's own float type as the reference computes (:55 img.copy())."""
     ycc = np.asarray(img)
+    if ycc.dtype.kind == "f" and not ycc.dtype.isnative:
+        # a byte-swapped float ('>f4' ...) holds the same values: compute on the native layout
+        ycc = ycc.astype(ycc.dtype.newbyteorder("="))
     if ycc.dtype not in _YCC_DTYPES:
-        # the reference's in-place "-= 0.5" (:58) refuses non-float arrays
+        # the reference's in-place "-= 0.5" (:58) refuses non-float arrays; longdouble has no
+        # type of its own here (the reference would compute in it)
         raise TypeError(f"expected a float16/32/64 array, got {ycc.dtype}")
     if ycc.ndim != 3 or ycc.shape[-1] != 3:
         raise ValueError(f"expected an (H, W, 3) array, got shape {ycc.shape}")

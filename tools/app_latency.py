@@ -55,6 +55,24 @@ def main():
     wm_img = W.embed_watermark(cover, png, True, cs)
     out["embed_watermark_ms"] = timed(lambda: W.embed_watermark(cover, png, True, cs))
     out["extract_watermark_ms"] = timed(lambda: W.extract_watermark(wm_img, cover, cs))
+    # where embed_watermark's time goes (its stages, each timed alone)
+    from thatsmyface_amd import _lib
+    rgb = np.ascontiguousarray(np.asarray(cover.convert("RGB"), dtype=np.uint8))
+    wimg = Image.open(io.BytesIO(png))
+    nbh, nbw = a.height // a.block, a.width // a.block
+    tile = np.ascontiguousarray(np.asarray(W.resize_watermark(wimg, nbh, nbw, True), dtype=np.uint8))
+    host_out = np.empty_like(rgb)
+    L = _lib.load()
+    stages = {
+        "convert_rgb": lambda: cover.convert("RGB"),
+        "asarray": lambda: np.ascontiguousarray(np.asarray(cover, dtype=np.uint8)),
+        "png_decode": lambda: Image.open(io.BytesIO(png)).convert("L"),
+        "resize_watermark": lambda: W.resize_watermark(wimg, nbh, nbw, True),
+        "tmfwm_embed_host": lambda: _lib.check(L.tmfwm_embed(rgb.ctypes.data, 1, a.height, a.width, rgb.size, tile.ctypes.data,
+                                                             a.block, 0.1, host_out.ctypes.data, _lib.MEM_HOST, None), "embed"),
+        "fromarray": lambda: Image.fromarray(host_out),
+    }
+    out["embed_stages_ms"] = {k: timed(f) for k, f in stages.items()}
     dev = torch.device("cuda", 0)
     fr = torch.from_numpy(np.asarray(cover)[None].copy()).to(dev)
     tile = batch.synth_tile(a.height // a.block, a.width // a.block, device=dev)
