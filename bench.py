@@ -64,6 +64,9 @@ def parse(argv=None):
                         "(the oracle's dgesdd route, ~1 s per 4K frame per 16 cores; 0 = skip)")
     p.add_argument("--pg-timeout", type=float, default=600.0,
                    help="seconds a rank may wait in a collective before the run fails (N > 1)")
+    p.add_argument("--route", default="hybrid", choices=["hybrid", "reference"],
+                   help="SVD route (DESIGN.md 3.5): hybrid = Jacobi + conditioning test (the throughput route); "
+                        "reference = the dgesdd route for every block (np.linalg.svd's arithmetic by construction)")
     p.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                    help="process-group backend for N > 1 (nccl = RCCL over xGMI; gloo only to rehearse "
                         "several ranks on one GPU)")
@@ -145,17 +148,18 @@ def spawn_ranks(args, argv, script=None) -> int:
     return subprocess.call(cmd, env=env)
 
 
-def gpu_kernels():
+def gpu_kernels(route="hybrid"):
     """The product path: libtmfwm.so's HIP kernels (thatsmyface_amd.batch)."""
     from thatsmyface_amd import batch
 
     return SimpleNamespace(
         synth_frames=lambda n, h, w, frame0, dev: batch.synth_frames(n, h, w, seed=batch.SEED_COVER, frame0=frame0, device=dev),
         synth_tile=lambda nbh, nbw, dev: batch.synth_tile(nbh, nbw, device=dev),
-        embed=lambda f, t, b, a, o: batch.embed_batch(f, t, b, a, out=o),
-        extract=lambda w_, o_, b, a, out: batch.extract_batch(w_, o_, b, a, out=out),
-        embed_stats=lambda f, t, b, a, o: (lambda st: (batch.embed_batch(f, t, b, a, out=o, stats=st), st)[1])({}),
-        embed_list_pass=batch.embed_list_pass,
+        embed=lambda f, t, b, a, o: batch.embed_batch(f, t, b, a, out=o, route=route),
+        extract=lambda w_, o_, b, a, out: batch.extract_batch(w_, o_, b, a, out=out, route=route),
+        embed_stats=lambda f, t, b, a, o: (lambda st: (batch.embed_batch(f, t, b, a, out=o, stats=st, route=route), st)[1])({}),
+        embed_list_pass=lambda b: batch.embed_list_pass(b) and route == "hybrid",
+        route=route,
     )
 
 
@@ -296,7 +300,7 @@ def run(args, kernels=None, device=None):
             dist.init_process_group("nccl", device_id=dev, timeout=timeout)
         else:
             dist.init_process_group("gloo", timeout=timeout)
-    K = kernels or gpu_kernels()
+    K = kernels or gpu_kernels(getattr(args, "route", "hybrid"))
     sync = torch.cuda.synchronize if on_gpu else (lambda: None)
 
     # distinct physical devices across ranks
@@ -517,15 +521,17 @@ def run(args, kernels=None, device=None):
                 "width": W,
                 "block": b,
                 "alpha": alpha,
+                "svd_route": getattr(args, "route", "hybrid"),
                 "parallelism": ("single GPU" if world == 1 else
                                 f"frame shards x{world}, {'RCCL' if args.backend == 'nccl' else 'gloo'} tile broadcast"),
             },
             "roofline": {
                 "bound": "hbm",
                 "kernel": f"embed_kernel<{b}>",
-                "launch": f"one tmfwm_embed call: embed_kernel<{b}> strip pass"
-                          + (" + list pass" if getattr(K, "embed_list_pass", lambda _b: False)(b) else "")
-                          + f" + embed_fixup_kernel<{b}> (dgesdd route)",
+                "launch": (f"one tmfwm_embed call: embed_kernel<{b}> strip pass"
+                           + (" + list pass" if getattr(K, "embed_list_pass", lambda _b: False)(b) else "")
+                           + f" + embed_fixup_kernel<{b}> (dgesdd route)") if getattr(K, "route", "hybrid") == "hybrid" else
+                          f"one tmfwm_embed_route call, TMFWM_ROUTE_REFERENCE: embed_fixup_kernel<{b}> (dgesdd route) on every block",
                 "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",

@@ -45,6 +45,12 @@ extern "C" {
 #define TMFWM_MEM_HOST 0
 #define TMFWM_MEM_DEVICE 1
 
+/* SVD routes of embed / extract (tmfwm_embed_route, tmfwm_extract_route) */
+#define TMFWM_ROUTE_HYBRID 0    /* Jacobi on every block, the dgesdd route for the blocks the
+                                   conditioning test flags (the throughput route: tmfwm_embed) */
+#define TMFWM_ROUTE_REFERENCE 1 /* the dgesdd route -- np.linalg.svd's own arithmetic -- for every
+                                   block: the reference's bytes by construction */
+
 #define TMFWM_OK 0
 #define TMFWM_ERR_INVALID (-22)     /* bad argument (EINVAL) */
 #define TMFWM_ERR_NOMEM (-12)       /* device allocation failed (ENOMEM) */
@@ -101,6 +107,18 @@ int tmfwm_embed_ex(const uint8_t *rgb, int64_t n_frames, int32_t height, int32_t
                    int64_t *n_lapack_blocks);
 
 /*
+ * tmfwm_embed_ex with an explicit SVD route (ABI 7): TMFWM_ROUTE_HYBRID is tmfwm_embed_ex;
+ * TMFWM_ROUTE_REFERENCE sends every block through the dgesdd route (LAPACK dgesdd + the
+ * OpenBLAS kernels numpy calls, restated operation by operation), so each output byte is
+ * computed by the reference's own arithmetic rather than agreeing with it up to the
+ * hybrid route's measured rounding-coincidence rate.  About two orders of magnitude less
+ * throughput than the hybrid route; *n_lapack_blocks then counts every block.
+ */
+int tmfwm_embed_route(const uint8_t *rgb, int64_t n_frames, int32_t height, int32_t width, int64_t frame_stride,
+                      const uint8_t *wm_tile, int32_t block, double alpha, uint8_t *out, int32_t mem_kind, void *hip_stream,
+                      int32_t route, int64_t *n_lapack_blocks);
+
+/*
  * Extract: replaces the body of extract_watermark() (watermarking.py:246-292):
  * luma of both images, per-block sigma_1 of the DCT of each, (s_w - s_o)/alpha
  * in float32, clip to [0,1], *255, truncation.  Both images have the same
@@ -116,6 +134,12 @@ int tmfwm_extract(const uint8_t *wm_rgb, const uint8_t *orig_rgb, int64_t n_fram
 int tmfwm_extract_ex(const uint8_t *wm_rgb, const uint8_t *orig_rgb, int64_t n_frames, int32_t height, int32_t width,
                      int64_t frame_stride, int32_t block, double alpha, uint8_t *out_tiles, int32_t mem_kind,
                      void *hip_stream, int64_t *n_lapack_blocks);
+
+/* tmfwm_extract_ex with an explicit SVD route (ABI 7): TMFWM_ROUTE_REFERENCE computes both
+ * sigma_1 of every block on the dgesdd route instead of certifying the Jacobi enclosure. */
+int tmfwm_extract_route(const uint8_t *wm_rgb, const uint8_t *orig_rgb, int64_t n_frames, int32_t height, int32_t width,
+                        int64_t frame_stride, int32_t block, double alpha, uint8_t *out_tiles, int32_t mem_kind,
+                        void *hip_stream, int32_t route, int64_t *n_lapack_blocks);
 
 /*
  * Multi-GPU embed / extract for callers without torch.distributed (one process drives

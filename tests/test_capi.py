@@ -58,6 +58,15 @@ def test_argument_validation_before_device():
     with pytest.raises(ValueError):  # alpha NaN
         _lib.check(L.tmfwm_embed(p(a), 1, 16, 16, a.size, p(t), 8, float("nan"), p(o), _lib.MEM_HOST, None), "embed")
     assert "frame_stride" in _lib.last_error() or "alpha" in _lib.last_error()
+    for bad_route in (-1, 2):  # TMFWM_ROUTE_HYBRID / _REFERENCE only
+        with pytest.raises(ValueError, match="route"):
+            _lib.check(L.tmfwm_embed_route(p(a), 1, 16, 16, a.size, p(t), 8, 0.1, p(o), _lib.MEM_HOST, None, bad_route, None), "e")
+        with pytest.raises(ValueError, match="route"):
+            _lib.check(L.tmfwm_extract_route(p(a), p(a), 1, 16, 16, a.size, 8, 0.1, p(t), _lib.MEM_HOST, None, bad_route, None), "x")
+    assert [L.tmfwm_embed_list_pass(k) for k in (4, 6, 8, 10, 12, 14, 16, 7, 18)] == [0, 0, 1, 0, 0, 0, 0, 0, 0]
+    with pytest.raises(ValueError):
+        _lib.route_code("exact")
+    assert (_lib.route_code("hybrid"), _lib.route_code("reference")) == (_lib.ROUTE_HYBRID, _lib.ROUTE_REFERENCE) == (0, 1)
 
 
 @pytest.mark.skipif(_lib.device_count() > 0, reason="CPU-only check")

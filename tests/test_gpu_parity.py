@@ -28,6 +28,14 @@ def dev():
     return torch.device("cuda", 0)
 
 
+# the oracle route the single-image drop-in's default SVD route corresponds to (constants.SVD_ROUTE:
+# "reference" -> the oracle's dgesdd route, "hybrid" -> the oracle's default hybrid route)
+def _dropin_oracle_route():
+    from thatsmyface_amd.constants import SVD_ROUTE
+
+    return {"reference": "lapack", "hybrid": None}[SVD_ROUTE]
+
+
 def _u8(seed, shape):
     return np.random.default_rng(seed).integers(0, 256, shape, dtype=np.uint8)
 
@@ -220,7 +228,7 @@ def test_golden_cases_dropin_gpu(dev, golden):
         assert np.array_equal(np.asarray(W.resize_watermark(wm, e.shape[0] // m["block"], e.shape[1] // m["block"],
                                                             m["preserve_ratio"])), cases[f"{name}/tile"]), name
         rgb = np.asarray(cov.convert("RGB"))
-        assert np.array_equal(e, O.embed_frame(rgb, cases[f"{name}/tile"], m["block"], m["alpha"])), name
+        assert np.array_equal(e, O.embed_frame(rgb, cases[f"{name}/tile"], m["block"], m["alpha"], route=_dropin_oracle_route())), name
         assert np.array_equal(e, cases[f"{name}/embed"]), name
         ex = W.extract_watermark(Image.fromarray(cases[f"{name}/embed"]), cov, settings)
         assert ex.mode == "L"
@@ -531,10 +539,11 @@ def test_call_site_patterns(dev, monkeypatch):
     b_ = MW.embed_watermark(img, watermark_data, True)  # watermarking_embed_test.py:102
     assert np.array_equal(np.asarray(a), np.asarray(b_))
     tile = O.prepare_tile(np.asarray(qr), 200 // 8, 264 // 8, True)
-    assert np.array_equal(np.asarray(a), O.embed_frame(np.asarray(img), tile, 8, 0.1))
+    route = _dropin_oracle_route()
+    assert np.array_equal(np.asarray(a), O.embed_frame(np.asarray(img), tile, 8, 0.1, route=route))
     x1 = MW.extract_watermark(a, img)  # extract_watermark_page.py:293-296, watermarking_extract_test.py:62
     assert x1.mode == "L" and x1.size == (264 // 8, 200 // 8)
-    assert np.array_equal(np.asarray(x1), O.extract_frame(np.asarray(a), np.asarray(img), 8, 0.1))
+    assert np.array_equal(np.asarray(x1), O.extract_frame(np.asarray(a), np.asarray(img), 8, 0.1, route=route))
 
 
 def test_config1_batch_256_1080p(dev):
@@ -622,11 +631,12 @@ def test_threads_dropin_gpu(dev):
 
     with ThreadPoolExecutor(8) as ex:
         res = list(ex.map(work, jobs))
+    route = _dropin_oracle_route()
     for (i, b, rgb, wm, alpha), (e, x) in zip(jobs, res):
         tile = O.prepare_tile(wm, rgb.shape[0] // b, rgb.shape[1] // b, i % 2 == 0)
-        ref = O.embed_frame(rgb, tile, b, alpha)
+        ref = O.embed_frame(rgb, tile, b, alpha, route=route)
         assert np.array_equal(e, ref), i
-        assert np.array_equal(x, O.extract_frame(ref, rgb, b, alpha)), i
+        assert np.array_equal(x, O.extract_frame(ref, rgb, b, alpha, route=route)), i
 
 
 def test_overlapping_buffers_refused(dev):
@@ -644,6 +654,48 @@ def test_overlapping_buffers_refused(dev):
     with pytest.raises(ValueError, match="overlaps"):
         _lib.check(L.tmfwm_extract(buf.data_ptr(), buf.data_ptr(), 1, h, w, h * w * 3, b, 0.1, buf.data_ptr() + 5,
                                    _lib.MEM_DEVICE, st), "extract")
+
+
+@pytest.mark.parametrize("b", [4, 6, 8, 10, 12, 14, 16])
+def test_reference_route_vs_oracle_lapack(dev, b):
+    """TMFWM_ROUTE_REFERENCE: every block on the dgesdd route (np.linalg.svd's arithmetic) --
+    bytes equal to the oracle's lapack route on noise, camera-like and binary QR covers (the
+    near-tie covers where the Jacobi route alone disagrees), for embed and extract, at every
+    block size; frame sizes with remainders exercise the edge pixels."""
+    from golden.gen_golden import cover
+    from lapack_path import photo_cover
+
+    from thatsmyface_amd import batch
+
+    H, W = 12 * b + 5, 20 * b + 3
+    covers = [_u8(300 + b, (H, W, 3)), photo_cover(H, W, 301 + b), np.ascontiguousarray(cover("qr", H, W, 302 + b))]
+    host = np.stack(covers)
+    t = _u8(303 + b, (H // b, W // b))
+    fr = torch.from_numpy(host).to(dev)
+    st = {}
+    out = batch.embed_batch(fr, torch.from_numpy(t).to(dev), b, 0.1, route="reference", stats=st)
+    assert st["lapack_blocks"] == len(covers) * (H // b) * (W // b)
+    ext = batch.extract_batch(out, fr, b, 0.1, route="reference").cpu().numpy()
+    out = out.cpu().numpy()
+    for f in range(len(covers)):
+        ref = O.embed_frame(host[f], t, b, 0.1, route="lapack")
+        assert np.array_equal(out[f], ref), (b, f)
+        assert np.array_equal(ext[f], O.extract_frame(ref, host[f], b, 0.1, route="lapack")), (b, f)
+
+
+def test_reference_route_golden_dropin_gpu(dev, golden, golden_blocks, golden_alpha):
+    """The drop-in with svd_route="reference" on every golden case (the reference's own bytes)."""
+    from thatsmyface_amd import watermarking as W
+
+    for cases, meta in (golden, golden_blocks, golden_alpha):
+        for name, m in meta["cases"].items():
+            cov = _cover_image(cases[f"{name}/cover"])
+            wm = Image.fromarray(cases[f"{name}/wm"], "L")
+            settings = {"block_size": m["block"], "alpha": m["alpha"], "svd_route": "reference"}
+            e = np.asarray(W.embed_watermark(cov, wm, m["preserve_ratio"], settings))
+            assert np.array_equal(e, cases[f"{name}/embed"]), name
+            ex = W.extract_watermark(Image.fromarray(cases[f"{name}/embed"]), cov, settings)
+            assert np.array_equal(np.asarray(ex), cases[f"{name}/extract"]), name
 
 
 def test_nonconvergence_reported_by_synchronising_calls(dev, monkeypatch):

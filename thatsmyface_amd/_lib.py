@@ -26,6 +26,22 @@ ERR_UNSUPPORTED = -95
 ERR_NODEVICE = -19
 ERR_NODATA = -61
 
+ROUTE_HYBRID = 0  # TMFWM_ROUTE_*: the SVD route of embed / extract (include/tmfwm.h)
+ROUTE_REFERENCE = 1
+ROUTES = {"hybrid": ROUTE_HYBRID, "reference": ROUTE_REFERENCE}
+
+
+def route_code(route) -> int:
+    """"hybrid" / "reference" (or the TMFWM_ROUTE_* value) -> the ABI's route value."""
+    if isinstance(route, str):
+        if route not in ROUTES:
+            raise ValueError(f"route must be one of {sorted(ROUTES)}, got {route!r}")
+        return ROUTES[route]
+    if route not in (ROUTE_HYBRID, ROUTE_REFERENCE):
+        raise ValueError(f"route {route!r}")
+    return int(route)
+
+
 DT_F16 = 1
 DT_F32 = 2
 DT_F64 = 3
@@ -47,6 +63,8 @@ SIGNATURES = {
     "tmfwm_embed_list_pass": (ctypes.c_int, [ctypes.c_int32]),
     "tmfwm_embed_ex": (ctypes.c_int, [_VP, _I64, _I32, _I32, _I64, _VP, _I32, _D, _VP, _I32, _VP, _VP]),
     "tmfwm_extract_ex": (ctypes.c_int, [_VP, _VP, _I64, _I32, _I32, _I64, _I32, _D, _VP, _I32, _VP, _VP]),
+    "tmfwm_embed_route": (ctypes.c_int, [_VP, _I64, _I32, _I32, _I64, _VP, _I32, _D, _VP, _I32, _VP, _I32, _VP]),
+    "tmfwm_extract_route": (ctypes.c_int, [_VP, _VP, _I64, _I32, _I32, _I64, _I32, _D, _VP, _I32, _VP, _I32, _VP]),
     "tmfwm_embed_multi": (ctypes.c_int, [_VP, _I64, _I32, _I32, _I64, _VP, _I32, _D, _VP, _VP, _I32, _VP]),
     "tmfwm_extract_multi": (ctypes.c_int, [_VP, _VP, _I64, _I32, _I32, _I64, _I32, _D, _VP, _VP, _I32, _VP]),
     "tmfwm_rgb_to_ycbcr": (ctypes.c_int, [_VP, _I64, _VP, _I32, _VP]),

@@ -45,10 +45,13 @@ def embed_list_pass(block: int) -> bool:
 
 
 def embed_batch(frames: torch.Tensor, wm_tile: torch.Tensor, block: int = 8, alpha: float = 0.1,
-                out: torch.Tensor | None = None, stream=None, stats: dict | None = None) -> torch.Tensor:
+                out: torch.Tensor | None = None, stream=None, stats: dict | None = None,
+                route: str = "hybrid") -> torch.Tensor:
     """Embed one watermark tile into every frame (watermarking.py:135 per frame).
     stats (optional dict) receives "lapack_blocks": the blocks redone on the dgesdd route;
-    asking for it synchronises the stream."""
+    asking for it synchronises the stream.  route: "hybrid" (Jacobi + the dgesdd route for
+    the flagged blocks, the throughput route) or "reference" (the dgesdd route for every
+    block: np.linalg.svd's arithmetic by construction)."""
     _check_frames(frames, "frames")
     n, h, w, _ = frames.shape
     if block not in SUPPORTED_BLOCK_SIZES:
@@ -65,8 +68,9 @@ def embed_batch(frames: torch.Tensor, wm_tile: torch.Tensor, block: int = 8, alp
     cnt, ptr = _count_ptr(stats)
     with torch.cuda.device(frames.device):
         L = _lib.load()
-        _lib.check(L.tmfwm_embed_ex(frames.data_ptr(), n, h, w, h * w * 3, wm_tile.data_ptr(), block, float(alpha),
-                                    out.data_ptr(), _lib.MEM_DEVICE, _stream(stream), ptr), "embed_batch")
+        _lib.check(L.tmfwm_embed_route(frames.data_ptr(), n, h, w, h * w * 3, wm_tile.data_ptr(), block, float(alpha),
+                                       out.data_ptr(), _lib.MEM_DEVICE, _stream(stream), _lib.route_code(route), ptr),
+                   "embed_batch")
     if stats is not None:
         stats["lapack_blocks"] = int(cnt.value)
         stats["list_pass_blocks"] = int(L.tmfwm_last_list_pass_blocks())
@@ -74,9 +78,11 @@ def embed_batch(frames: torch.Tensor, wm_tile: torch.Tensor, block: int = 8, alp
 
 
 def extract_batch(wframes: torch.Tensor, oframes: torch.Tensor, block: int = 8, alpha: float = 0.1,
-                  out: torch.Tensor | None = None, stream=None, stats: dict | None = None) -> torch.Tensor:
+                  out: torch.Tensor | None = None, stream=None, stats: dict | None = None,
+                  route: str = "hybrid") -> torch.Tensor:
     """Extract the watermark tile of every frame pair (watermarking.py:224 per pair).
-    stats (optional dict) receives "lapack_blocks" (synchronises the stream)."""
+    stats (optional dict) receives "lapack_blocks" (synchronises the stream); route as
+    embed_batch's."""
     _check_frames(wframes, "wframes")
     _check_frames(oframes, "oframes")
     if wframes.shape != oframes.shape:
@@ -89,8 +95,9 @@ def extract_batch(wframes: torch.Tensor, oframes: torch.Tensor, block: int = 8, 
     cnt, ptr = _count_ptr(stats)
     with torch.cuda.device(wframes.device):
         L = _lib.load()
-        _lib.check(L.tmfwm_extract_ex(wframes.data_ptr(), oframes.data_ptr(), n, h, w, h * w * 3, block, float(alpha),
-                                      out.data_ptr(), _lib.MEM_DEVICE, _stream(stream), ptr), "extract_batch")
+        _lib.check(L.tmfwm_extract_route(wframes.data_ptr(), oframes.data_ptr(), n, h, w, h * w * 3, block, float(alpha),
+                                         out.data_ptr(), _lib.MEM_DEVICE, _stream(stream), _lib.route_code(route), ptr),
+                   "extract_batch")
     if stats is not None:
         stats["lapack_blocks"] = int(cnt.value)
         stats["list_pass_blocks"] = int(L.tmfwm_last_list_pass_blocks())

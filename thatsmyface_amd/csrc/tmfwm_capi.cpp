@@ -3,6 +3,7 @@
 // kernel launchers of tmfwm_kernels.hip.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdarg>
 #include <cstdint>
@@ -192,8 +193,24 @@ struct Chunks {
     }
 };
 
-// copy the per-chunk counts back (synchronises the stream) and sum them; dcounts holds the
-// chunks' dgesdd-route counts, then their non-convergence counts, then their list-pass counts
+// sum the per-chunk counts h[0 .. 3*nchunks) (dgesdd-route, non-convergence, list-pass)
+int sum_host_counts(const uint32_t *h, int64_t nchunks, int64_t *out)
+{
+    int64_t t = 0, bad = 0, slow = 0;
+    for (int64_t c = 0; c < nchunks; ++c) {
+        t += h[c];
+        bad += h[nchunks + c];
+        slow += h[2 * nchunks + c];
+    }
+    if (out) *out = t;
+    t_list_pass = slow;
+    if (bad)
+        return fail(TMFWM_ERR_HIP, "dgesdd route: dbdsqr did not converge on %lld block(s) (np.linalg.svd raises LinAlgError there)",
+                    (long long)bad);
+    return 0;
+}
+
+// copy the per-chunk counts back (synchronises the stream) and sum them
 int sum_counts(const uint32_t *dcounts, int64_t nchunks, hipStream_t st, int64_t *out)
 {
     std::vector<uint32_t> h((size_t)(3 * nchunks));
@@ -205,18 +222,7 @@ int sum_counts(const uint32_t *dcounts, int64_t nchunks, hipStream_t st, int64_t
             return fail(TMFWM_ERR_HIP, "reading the dgesdd-route counts failed: %s", hipGetErrorString(e));
         }
     }
-    int64_t t = 0, bad = 0, slow = 0;
-    for (int64_t c = 0; c < nchunks; ++c) {
-        t += h[(size_t)c];
-        bad += h[(size_t)(nchunks + c)];
-        slow += h[(size_t)(2 * nchunks + c)];
-    }
-    if (out) *out = t;
-    t_list_pass = slow;
-    if (bad)
-        return fail(TMFWM_ERR_HIP, "dgesdd route: dbdsqr did not converge on %lld block(s) (np.linalg.svd raises LinAlgError there)",
-                    (long long)bad);
-    return 0;
+    return sum_host_counts(h.data(), nchunks, out);
 }
 
 }  // namespace
@@ -243,14 +249,14 @@ int check_frames(int64_t n, int32_t H, int32_t W, int64_t stride, int32_t block)
 // when `check` is set (the host-memory calls, which synchronise anyway): a dbdsqr that did not
 // converge then fails the call (np.linalg.svd raises LinAlgError there).  An asynchronous
 // device-memory call without a count pointer is not checked (include/tmfwm.h).
-int run_embed(EmbedArgs a, hipStream_t st, int64_t *n_lapack, bool check)
+int run_embed(EmbedArgs a, hipStream_t st, int64_t *n_lapack, bool check, uint32_t *sink = nullptr, int route = TMFWM_ROUTE_HYBRID)
 {
     Chunks ch;
     ch.plan(a.nframes, (int64_t)a.nbh * a.nbw);
     DevBuf list, slow, counts;
     if (ch.cap > 0) {
         if (int rc = list.alloc((size_t)ch.cap * 4, st, "dgesdd-route block list")) return rc;
-        if (embed_defers(a.block))
+        if (embed_defers(a.block) && route == TMFWM_ROUTE_HYBRID)
             if (int rc = slow.alloc((size_t)ch.cap * 4, st, "list-pass block list")) return rc;
         // per chunk: dgesdd-route count, non-convergence count, list-pass count
         if (int rc = counts.alloc((size_t)ch.n * 12, st, "block-list counts")) return rc;
@@ -258,6 +264,7 @@ int run_embed(EmbedArgs a, hipStream_t st, int64_t *n_lapack, bool check)
     }
     if (ch.cap == 0) {  // no full block: colour round trip only
         TMF_HIP(launch_embed(a, st));
+        if (sink) std::fill(sink, sink + 3 * ch.n, 0u);
         if (n_lapack) {
             *n_lapack = 0;
             t_list_pass = 0;
@@ -275,19 +282,30 @@ int run_embed(EmbedArgs a, hipStream_t st, int64_t *n_lapack, bool check)
         k.fb_bad = static_cast<uint32_t *>(counts.p) + ch.n + c;
         k.slow_list = static_cast<uint32_t *>(slow.p);  // null unless embed_defers(block)
         k.slow_count = static_cast<uint32_t *>(counts.p) + 2 * ch.n + c;
-        TMF_HIP(launch_embed(k, st));
+        if (route == TMFWM_ROUTE_REFERENCE) {  // every block on the dgesdd route; the edges as always
+            TMF_HIP(launch_edges(k.src, k.dst, k.nframes, k.H, k.W, k.frame_stride, k.block, st));
+            TMF_HIP(launch_list_all(k.fb_list, k.fb_count, k.nframes * ch.per_frame, st));
+        } else {
+            TMF_HIP(launch_embed(k, st));
+        }
         TMF_HIP(launch_embed_fixup(k, k.fb_list, k.fb_count, k.nframes * ch.per_frame, st));
         if (force_nonconv()) TMF_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(k.fb_bad), 1, 1, st));
+    }
+    if (sink) {  // tmf::embed_device_async / extract_device_async: the caller sums after its sync
+        TMF_HIP(hipMemcpyAsync(sink, counts.p, (size_t)ch.n * 12, hipMemcpyDeviceToHost, st));
+        return 0;
     }
     if (n_lapack || check) return sum_counts(static_cast<const uint32_t *>(counts.p), ch.n, st, n_lapack);
     return 0;
 }
 
-int run_extract(ExtractArgs a, hipStream_t st, int64_t *n_lapack, bool check)
+int run_extract(ExtractArgs a, hipStream_t st, int64_t *n_lapack, bool check, uint32_t *sink = nullptr,
+                int route = TMFWM_ROUTE_HYBRID)
 {
     Chunks ch;
     ch.plan(a.nframes, (int64_t)a.nbh * a.nbw);
     if (ch.cap == 0) {
+        if (sink) std::fill(sink, sink + 3 * ch.n, 0u);
         if (n_lapack) {
             *n_lapack = 0;
             t_list_pass = 0;
@@ -296,7 +314,8 @@ int run_extract(ExtractArgs a, hipStream_t st, int64_t *n_lapack, bool check)
     }
     DevBuf list, slow, counts;
     if (int rc = list.alloc((size_t)ch.cap * 4, st, "dgesdd-route block list")) return rc;
-    if (int rc = slow.alloc((size_t)ch.cap * 4, st, "list-pass block list")) return rc;
+    if (route == TMFWM_ROUTE_HYBRID)
+        if (int rc = slow.alloc((size_t)ch.cap * 4, st, "list-pass block list")) return rc;
     if (int rc = counts.alloc((size_t)ch.n * 12, st, "block-list counts")) return rc;  // as run_embed's
     TMF_HIP(hipMemsetAsync(counts.p, 0, (size_t)ch.n * 12, st));
     for (int64_t c = 0; c < ch.n; ++c) {
@@ -311,13 +330,92 @@ int run_extract(ExtractArgs a, hipStream_t st, int64_t *n_lapack, bool check)
         k.fb_bad = static_cast<uint32_t *>(counts.p) + ch.n + c;
         k.slow_list = static_cast<uint32_t *>(slow.p);
         k.slow_count = static_cast<uint32_t *>(counts.p) + 2 * ch.n + c;
-        TMF_HIP(launch_extract(k, st));
+        if (route == TMFWM_ROUTE_REFERENCE) TMF_HIP(launch_list_all(k.fb_list, k.fb_count, k.nframes * ch.per_frame, st));
+        else TMF_HIP(launch_extract(k, st));
         TMF_HIP(launch_extract_fixup(k, k.fb_list, k.fb_count, k.nframes * ch.per_frame, st));
         if (force_nonconv()) TMF_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(k.fb_bad), 1, 1, st));
+    }
+    if (sink) {  // tmf::embed_device_async / extract_device_async: the caller sums after its sync
+        TMF_HIP(hipMemcpyAsync(sink, counts.p, (size_t)ch.n * 12, hipMemcpyDeviceToHost, st));
+        return 0;
     }
     if (n_lapack || check) return sum_counts(static_cast<const uint32_t *>(counts.p), ch.n, st, n_lapack);
     return 0;
 }
+EmbedArgs embed_args(int64_t n, int32_t H, int32_t W, int64_t stride, int32_t block, double alpha)
+{
+    EmbedArgs a{};
+    a.nframes = n;
+    a.frame_stride = stride;
+    a.H = H;
+    a.W = W;
+    a.block = block;
+    a.nbh = H / block;
+    a.nbw = W / block;
+    a.alpha = alpha;
+    return a;
+}
+
+ExtractArgs extract_args(int64_t n, int32_t H, int32_t W, int64_t stride, int32_t block, double alpha)
+{
+    ExtractArgs a{};
+    a.nframes = n;
+    a.frame_stride = stride;
+    a.tile_stride = (int64_t)(H / block) * (W / block);
+    a.H = H;
+    a.W = W;
+    a.block = block;
+    a.nbh = H / block;
+    a.nbw = W / block;
+    a.alpha32 = (float)alpha;
+    return a;
+}
+
+bool dev_aligned(const void *p, const void *q, int64_t stride, int W)
+{
+    return ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(q)) % 4 == 0) && stride % 4 == 0 && W % 4 == 0;
+}
+
+int64_t count_chunks(int64_t nframes, int H, int W, int block)
+{
+    Chunks ch;
+    ch.plan(nframes, (int64_t)(H / block) * (W / block));
+    return ch.n;
+}
+
+int embed_device_async(const uint8_t *src, int64_t n, int H, int W, int64_t stride, const uint8_t *tile, int block,
+                       double alpha, uint8_t *dst, hipStream_t st, uint32_t *sink, int route)
+{
+    if (int rc = ::check_frames(n, H, W, stride, block)) return rc;
+    if (n == 0 || H == 0 || W == 0) {
+        std::fill(sink, sink + 3 * count_chunks(n, H, W, block), 0u);
+        return 0;
+    }
+    EmbedArgs a = embed_args(n, H, W, stride, block, alpha);
+    a.src = src;
+    a.dst = dst;
+    a.wm = tile;
+    a.aligned = dev_aligned(src, dst, stride, W);
+    return run_embed(a, st, nullptr, false, sink, route);
+}
+
+int extract_device_async(const uint8_t *wsrc, const uint8_t *osrc, int64_t n, int H, int W, int64_t stride, int block,
+                         double alpha, uint8_t *out, hipStream_t st, uint32_t *sink, int route)
+{
+    if (int rc = ::check_frames(n, H, W, stride, block)) return rc;
+    if (n == 0 || (H / block) * (W / block) == 0) {
+        std::fill(sink, sink + 3 * count_chunks(n, H, W, block), 0u);
+        return 0;
+    }
+    ExtractArgs a = extract_args(n, H, W, stride, block, alpha);
+    a.wsrc = wsrc;
+    a.osrc = osrc;
+    a.out = out;
+    a.aligned = dev_aligned(wsrc, osrc, stride, W);
+    return run_extract(a, st, nullptr, false, sink, route);
+}
+
+int sum_sink(const uint32_t *sink, int64_t nchunks, int64_t *lapack) { return sum_host_counts(sink, nchunks, lapack); }
 }  // namespace tmf
 
 extern "C" {
@@ -340,11 +438,12 @@ int tmfwm_device_count(void)
     return n;
 }
 
-int tmfwm_embed_ex(const uint8_t *rgb, int64_t n_frames, int32_t height, int32_t width, int64_t frame_stride,
-                   const uint8_t *wm_tile, int32_t block, double alpha, uint8_t *out, int32_t mem_kind, void *hip_stream,
-                   int64_t *n_lapack_blocks)
+int tmfwm_embed_route(const uint8_t *rgb, int64_t n_frames, int32_t height, int32_t width, int64_t frame_stride,
+                      const uint8_t *wm_tile, int32_t block, double alpha, uint8_t *out, int32_t mem_kind, void *hip_stream,
+                      int32_t route, int64_t *n_lapack_blocks)
 {
     t_err.clear();
+    if (route != TMFWM_ROUTE_HYBRID && route != TMFWM_ROUTE_REFERENCE) return fail(TMFWM_ERR_INVALID, "route %d", route);
     if (n_lapack_blocks) {
         *n_lapack_blocks = 0;
         t_list_pass = 0;  // this call's count from here on (an early return leaves 0)
@@ -357,15 +456,7 @@ int tmfwm_embed_ex(const uint8_t *rgb, int64_t n_frames, int32_t height, int32_t
     const int64_t fbytes = (int64_t)height * width * 3;
     const size_t span = span_bytes(n_frames, frame_stride, fbytes), tbytes = (size_t)nbh * nbw;
     hipStream_t st = pick_stream(hip_stream);
-    tmf::EmbedArgs a{};
-    a.nframes = n_frames;
-    a.frame_stride = frame_stride;
-    a.H = height;
-    a.W = width;
-    a.block = block;
-    a.nbh = nbh;
-    a.nbw = nbw;
-    a.alpha = alpha;
+    tmf::EmbedArgs a = tmf::embed_args(n_frames, height, width, frame_stride, block, alpha);
     if (mem_kind == TMFWM_MEM_DEVICE) {
         if (int rc = check_device_ptr(rgb, "rgb")) return rc;
         if (int rc = check_device_ptr(out, "out")) return rc;
@@ -377,8 +468,8 @@ int tmfwm_embed_ex(const uint8_t *rgb, int64_t n_frames, int32_t height, int32_t
         a.src = rgb;
         a.dst = out;
         a.wm = wm_tile;
-        a.aligned = ((reinterpret_cast<uintptr_t>(rgb) | reinterpret_cast<uintptr_t>(out)) % 4 == 0) && frame_stride % 4 == 0 && width % 4 == 0;
-        return tmf::run_embed(a, st, n_lapack_blocks, false);
+        a.aligned = tmf::dev_aligned(rgb, out, frame_stride, width);
+        return tmf::run_embed(a, st, n_lapack_blocks, false, nullptr, route);
     }
     if (mem_kind != TMFWM_MEM_HOST) return fail(TMFWM_ERR_INVALID, "mem_kind %d", mem_kind);
     if (!rgb || !out || (tbytes && !wm_tile)) return fail(TMFWM_ERR_INVALID, "NULL host pointer");
@@ -392,7 +483,7 @@ int tmfwm_embed_ex(const uint8_t *rgb, int64_t n_frames, int32_t height, int32_t
     a.dst = static_cast<uint8_t *>(dout.p);
     a.wm = static_cast<const uint8_t *>(dwm.p);
     a.aligned = frame_stride % 4 == 0 && width % 4 == 0;
-    if (int rc = tmf::run_embed(a, st, n_lapack_blocks, true)) return rc;
+    if (int rc = tmf::run_embed(a, st, n_lapack_blocks, true, nullptr, route)) return rc;
     if (frame_stride == fbytes) {
         TMF_HIP(hipMemcpyAsync(out, dout.p, span, hipMemcpyDeviceToHost, st));
     } else {
@@ -404,17 +495,26 @@ int tmfwm_embed_ex(const uint8_t *rgb, int64_t n_frames, int32_t height, int32_t
     return 0;
 }
 
+int tmfwm_embed_ex(const uint8_t *rgb, int64_t n_frames, int32_t height, int32_t width, int64_t frame_stride,
+                   const uint8_t *wm_tile, int32_t block, double alpha, uint8_t *out, int32_t mem_kind, void *hip_stream,
+                   int64_t *n_lapack_blocks)
+{
+    return tmfwm_embed_route(rgb, n_frames, height, width, frame_stride, wm_tile, block, alpha, out, mem_kind, hip_stream,
+                             TMFWM_ROUTE_HYBRID, n_lapack_blocks);
+}
+
 int tmfwm_embed(const uint8_t *rgb, int64_t n_frames, int32_t height, int32_t width, int64_t frame_stride,
                 const uint8_t *wm_tile, int32_t block, double alpha, uint8_t *out, int32_t mem_kind, void *hip_stream)
 {
     return tmfwm_embed_ex(rgb, n_frames, height, width, frame_stride, wm_tile, block, alpha, out, mem_kind, hip_stream, nullptr);
 }
 
-int tmfwm_extract_ex(const uint8_t *wm_rgb, const uint8_t *orig_rgb, int64_t n_frames, int32_t height, int32_t width,
-                     int64_t frame_stride, int32_t block, double alpha, uint8_t *out_tiles, int32_t mem_kind, void *hip_stream,
-                     int64_t *n_lapack_blocks)
+int tmfwm_extract_route(const uint8_t *wm_rgb, const uint8_t *orig_rgb, int64_t n_frames, int32_t height, int32_t width,
+                        int64_t frame_stride, int32_t block, double alpha, uint8_t *out_tiles, int32_t mem_kind,
+                        void *hip_stream, int32_t route, int64_t *n_lapack_blocks)
 {
     t_err.clear();
+    if (route != TMFWM_ROUTE_HYBRID && route != TMFWM_ROUTE_REFERENCE) return fail(TMFWM_ERR_INVALID, "route %d", route);
     if (n_lapack_blocks) {
         *n_lapack_blocks = 0;
         t_list_pass = 0;  // this call's count from here on (an early return leaves 0)
@@ -428,16 +528,7 @@ int tmfwm_extract_ex(const uint8_t *wm_rgb, const uint8_t *orig_rgb, int64_t n_f
     const int64_t fbytes = (int64_t)height * width * 3;
     const size_t span = span_bytes(n_frames, frame_stride, fbytes);
     hipStream_t st = pick_stream(hip_stream);
-    tmf::ExtractArgs a{};
-    a.nframes = n_frames;
-    a.frame_stride = frame_stride;
-    a.tile_stride = tbytes;
-    a.H = height;
-    a.W = width;
-    a.block = block;
-    a.nbh = nbh;
-    a.nbw = nbw;
-    a.alpha32 = (float)alpha;
+    tmf::ExtractArgs a = tmf::extract_args(n_frames, height, width, frame_stride, block, alpha);
     if (mem_kind == TMFWM_MEM_DEVICE) {
         if (int rc = check_device_ptr(wm_rgb, "wm_rgb")) return rc;
         if (int rc = check_device_ptr(orig_rgb, "orig_rgb")) return rc;
@@ -448,8 +539,8 @@ int tmfwm_extract_ex(const uint8_t *wm_rgb, const uint8_t *orig_rgb, int64_t n_f
         a.wsrc = wm_rgb;
         a.osrc = orig_rgb;
         a.out = out_tiles;
-        a.aligned = ((reinterpret_cast<uintptr_t>(wm_rgb) | reinterpret_cast<uintptr_t>(orig_rgb)) % 4 == 0) && frame_stride % 4 == 0 && width % 4 == 0;
-        return tmf::run_extract(a, st, n_lapack_blocks, false);
+        a.aligned = tmf::dev_aligned(wm_rgb, orig_rgb, frame_stride, width);
+        return tmf::run_extract(a, st, n_lapack_blocks, false, nullptr, route);
     }
     if (mem_kind != TMFWM_MEM_HOST) return fail(TMFWM_ERR_INVALID, "mem_kind %d", mem_kind);
     if (!wm_rgb || !orig_rgb || !out_tiles) return fail(TMFWM_ERR_INVALID, "NULL host pointer");
@@ -463,10 +554,18 @@ int tmfwm_extract_ex(const uint8_t *wm_rgb, const uint8_t *orig_rgb, int64_t n_f
     a.osrc = static_cast<const uint8_t *>(dor.p);
     a.out = static_cast<uint8_t *>(dout.p);
     a.aligned = frame_stride % 4 == 0 && width % 4 == 0;
-    if (int rc = tmf::run_extract(a, st, n_lapack_blocks, true)) return rc;
+    if (int rc = tmf::run_extract(a, st, n_lapack_blocks, true, nullptr, route)) return rc;
     TMF_HIP(hipMemcpyAsync(out_tiles, dout.p, (size_t)(tbytes * n_frames), hipMemcpyDeviceToHost, st));
     TMF_HIP(hipStreamSynchronize(st));
     return 0;
+}
+
+int tmfwm_extract_ex(const uint8_t *wm_rgb, const uint8_t *orig_rgb, int64_t n_frames, int32_t height, int32_t width,
+                     int64_t frame_stride, int32_t block, double alpha, uint8_t *out_tiles, int32_t mem_kind, void *hip_stream,
+                     int64_t *n_lapack_blocks)
+{
+    return tmfwm_extract_route(wm_rgb, orig_rgb, n_frames, height, width, frame_stride, block, alpha, out_tiles, mem_kind,
+                               hip_stream, TMFWM_ROUTE_HYBRID, n_lapack_blocks);
 }
 
 int tmfwm_extract(const uint8_t *wm_rgb, const uint8_t *orig_rgb, int64_t n_frames, int32_t height, int32_t width,

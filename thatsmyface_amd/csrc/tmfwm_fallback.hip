@@ -45,6 +45,22 @@ hipError_t launch_extract_fixup(const ExtractArgs &a, const uint32_t *list, cons
     }
 }
 
+// The reference route (TMFWM_ROUTE_REFERENCE): every block of the launch on the dgesdd route.
+// The id list is the identity, written on the device (ids 0 .. n-1 and the count n).
+__global__ __launch_bounds__(256) void list_all_kernel(uint32_t *__restrict__ list, uint32_t *__restrict__ count, uint32_t n)
+{
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i < n) list[i] = i;
+    if (i == 0) *count = n;
+}
+
+hipError_t launch_list_all(uint32_t *list, uint32_t *count, int64_t n, hipStream_t st)
+{
+    if (n <= 0 || n > 0xFFFFFFFFll) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(list_all_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, list, count, (uint32_t)n);
+    return hipGetLastError();
+}
+
 // stage entry points (tmfwm_lapack_svd_blocks, tmfwm_lapack_nrm2): the same wave-parallel
 // route as the fixup passes, one 64-lane workgroup per block, the workspace in LDS
 __global__ __launch_bounds__(64) void lp_svd_blocks_kernel(const float *__restrict__ D, int64_t nb, int b, float *__restrict__ U,

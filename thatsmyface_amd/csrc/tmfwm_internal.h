@@ -60,6 +60,19 @@ int report(int code, const char *fmt, ...);  // sets this thread's tmfwm_last_er
 void clear_error();
 int check_frames(int64_t n, int32_t H, int32_t W, int64_t stride, int32_t block);
 
+// Device-memory embed / extract that never synchronise (tmfwm_multi.cpp's pipelined passes).
+// Instead of reading the per-chunk counts back, they go to `sink` -- pinned host memory of
+// 3 * count_chunks(...) uint32 entries: the chunks' dgesdd-route counts, then their dbdsqr
+// non-convergence counts, then their list-pass counts -- by a copy enqueued on the stream; the
+// caller sums them with sum_sink() once the stream is done.  Arguments as tmfwm_embed_ex /
+// tmfwm_extract_ex with TMFWM_MEM_DEVICE (checked the same way).
+int64_t count_chunks(int64_t nframes, int H, int W, int block);
+int embed_device_async(const uint8_t *src, int64_t n, int H, int W, int64_t stride, const uint8_t *tile, int block,
+                       double alpha, uint8_t *dst, hipStream_t st, uint32_t *sink, int route = TMFWM_ROUTE_HYBRID);
+int extract_device_async(const uint8_t *wsrc, const uint8_t *osrc, int64_t n, int H, int W, int64_t stride, int block,
+                         double alpha, uint8_t *out, hipStream_t st, uint32_t *sink, int route = TMFWM_ROUTE_HYBRID);
+int sum_sink(const uint32_t *sink, int64_t nchunks, int64_t *lapack);  // TMFWM_ERR_HIP on non-convergence
+
 hipError_t launch_embed(const EmbedArgs &a, hipStream_t st);
 bool embed_defers(int block);  // the strip pass of embed_kernel<block> can leave blocks to a list pass
 hipError_t launch_edges(const uint8_t *src, uint8_t *dst, int64_t nframes, int H, int W, int64_t frame_stride, int block, hipStream_t st);
@@ -71,6 +84,8 @@ hipError_t launch_dct2d_blocks(float *blocks, int64_t nb, int block, int inverse
 // second pass on the dgesdd route (tmfwm_fallback.hip); max_entries bounds the list
 hipError_t launch_embed_fixup(const EmbedArgs &a, const uint32_t *list, const uint32_t *count, int64_t max_entries, hipStream_t st);
 hipError_t launch_extract_fixup(const ExtractArgs &a, const uint32_t *list, const uint32_t *count, int64_t max_entries, hipStream_t st);
+// the reference route: list = 0 .. n-1, *count = n (every block of a launch on the dgesdd route)
+hipError_t launch_list_all(uint32_t *list, uint32_t *count, int64_t n, hipStream_t st);
 hipError_t launch_lapack_svd_blocks(const float *D, int64_t nb, int block, float *U, float *S, float *Vt, int want_v, int32_t *info,
                                     hipStream_t st);
 hipError_t launch_lapack_nrm2(const double *x, int64_t nvec, int n, int inc, double *out, hipStream_t st);

@@ -116,13 +116,56 @@ struct DeviceTile {
     hipEvent_t ready = nullptr;
 };
 
-// Frames per pass of a shard: device buffers of at most ~4 GiB (in + out) per shard.
+// Frames per pass of a shard: two pass slots of at most ~2 GiB each (inputs + outputs), so
+// that a pass's transfers overlap the neighbouring pass's kernels.
 int64_t pass_frames(int64_t frame_bytes)
 {
-    const int64_t budget = int64_t(2) << 30;
+    const int64_t budget = int64_t(1) << 30;
     const int64_t f = frame_bytes > 0 ? budget / frame_bytes : 1;
     return f < 1 ? 1 : f;
 }
+
+// Device staging buffers, kept per device across calls (an app batch loop calls the multi
+// entry points over and over; hipMalloc / hipFree of GiBs per call would cost more than a
+// pass).  A shard leases the buffers it needs and gives them back when it is done; the cache
+// holds them for the life of the process (at most two pass slots per concurrent shard).
+struct BufCache {
+    std::mutex mu;
+    std::multimap<int, std::pair<size_t, void *>> free;  // device -> (bytes, pointer)
+    static BufCache &get()
+    {
+        static BufCache c;
+        return c;
+    }
+    void *lease(int dev, size_t bytes)
+    {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            auto r = free.equal_range(dev);
+            for (auto it = r.first; it != r.second; ++it)
+                if (it->second.first >= bytes) {
+                    void *p = it->second.second;
+                    free.erase(it);
+                    return p;
+                }
+        }
+        void *p = nullptr;
+        if (hipMalloc(&p, bytes) != hipSuccess) {
+            (void)hipGetLastError();
+            return nullptr;
+        }
+        std::lock_guard<std::mutex> lk(mu);
+        sizes[p] = bytes;
+        return p;
+    }
+    void give_back(int dev, void *p)
+    {
+        if (!p) return;
+        std::lock_guard<std::mutex> lk(mu);
+        free.emplace(dev, std::make_pair(sizes[p], p));
+    }
+    std::map<void *, size_t> sizes;
+};
 
 int plan_shards(const int32_t *devices, int32_t n_shards, int64_t n_frames, std::vector<Shard> &sh, std::vector<DeviceTile> &uniq)
 {
@@ -231,38 +274,107 @@ int distribute_tile(const uint8_t *wm_tile, size_t tbytes, std::vector<DeviceTil
     return 0;
 }
 
-// One shard, on its own thread: passes of at most pass_frames() frames, each staged
-// host -> device, embedded / extracted on the device path of the ABI, copied back.
-template <typename Body>
-void run_shard(Shard &s, const DeviceTile &u, int64_t in_bytes, int64_t out_bytes, int n_inputs, Body body)
+// One shard, on its own thread: passes of at most pass_frames() frames in two alternating
+// slots.  Three streams: uploads, kernels (s.st), downloads.  Pass p's kernels wait for its
+// upload and for the download of pass p - 2 (which used the same output slot); its upload
+// waits for the kernels of pass p - 2 (same input slot).  The host thread enqueues pass p's
+// kernels before it copies pass p - 1 down and pass p + 1 up, so with pageable host memory
+// (each copy call returns once its data has been staged) the kernels of one pass run while
+// the neighbouring passes move over PCIe.  The per-pass counts (dgesdd-route blocks,
+// non-convergence) land in pinned host memory and are summed once the shard is done.
+template <typename Up, typename Kern, typename Down>
+void run_shard(Shard &s, const DeviceTile &u, int64_t in_bytes, int64_t out_bytes, int n_inputs, int H, int W, int block,
+               Up up, Kern kern, Down down)
 {
     auto fail_here = [&](int rc, const std::string &m) {
-        s.rc = rc;
-        s.err = m;
+        if (s.rc == 0) {
+            s.rc = rc;
+            s.err = m;
+        }
     };
     if (hipSetDevice(s.device) != hipSuccess) return fail_here(TMFWM_ERR_HIP, "hipSetDevice failed");
     const int64_t n = s.stop - s.start;
     if (n == 0) return;
     const int64_t per = std::min<int64_t>(n, pass_frames(in_bytes * n_inputs + out_bytes));
-    uint8_t *din = nullptr, *dout = nullptr;
-    hipError_t e = hipMalloc(&din, (size_t)(per * in_bytes * n_inputs));
-    if (e == hipSuccess) e = hipMalloc(&dout, (size_t)(per * out_bytes));
+    const int64_t npass = (n + per - 1) / per;
+    const size_t in_slot = (size_t)(per * in_bytes * n_inputs), out_slot = (size_t)(per * out_bytes);
+    const int64_t chunks_per_pass = tmf::count_chunks(per, H, W, block);  // a shorter last pass has no more
+    BufCache &bc = BufCache::get();
+    uint8_t *din[2] = {nullptr, nullptr}, *dout[2] = {nullptr, nullptr};
+    hipStream_t sup = nullptr, sdown = nullptr;
+    hipEvent_t up_done[2] = {}, kern_done[2] = {}, down_done[2] = {};
+    uint32_t *sink = nullptr;  // 3 * chunks_per_pass per pass, pinned
+    const size_t sink_n = (size_t)(3 * chunks_per_pass * npass);
+    auto cleanup = [&] {
+        for (hipStream_t x : {sup, s.st, sdown})
+            if (x) (void)hipStreamSynchronize(x);
+        for (int k = 0; k < 2; ++k) {
+            bc.give_back(s.device, din[k]);
+            bc.give_back(s.device, dout[k]);
+            for (hipEvent_t e : {up_done[k], kern_done[k], down_done[k]})
+                if (e) (void)hipEventDestroy(e);
+        }
+        if (sup) (void)hipStreamDestroy(sup);
+        if (sdown) (void)hipStreamDestroy(sdown);
+        if (sink) (void)hipHostFree(sink);
+        (void)hipGetLastError();
+    };
+    hipError_t e = hipSuccess;
+    for (int k = 0; k < (npass > 1 ? 2 : 1) && e == hipSuccess; ++k) {
+        din[k] = static_cast<uint8_t *>(bc.lease(s.device, in_slot));
+        dout[k] = static_cast<uint8_t *>(bc.lease(s.device, out_slot));
+        if (!din[k] || !dout[k]) e = hipErrorOutOfMemory;
+    }
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&sup, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&sdown, hipStreamNonBlocking);
+    for (int k = 0; k < 2 && e == hipSuccess; ++k)
+        for (hipEvent_t *ev : {&up_done[k], &kern_done[k], &down_done[k]})
+            if (e == hipSuccess) e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&sink), sink_n * 4, hipHostMallocDefault);
+    if (e == hipSuccess) std::fill(sink, sink + sink_n, 0u);
     if (e == hipSuccess) e = hipStreamWaitEvent(s.st, u.ready, 0);
     if (e != hipSuccess) {
-        (void)hipGetLastError();
-        if (din) (void)hipFree(din);
+        cleanup();
         return fail_here(e == hipErrorOutOfMemory ? TMFWM_ERR_NOMEM : TMFWM_ERR_HIP, std::string("shard setup: ") + hipGetErrorString(e));
     }
-    for (int64_t f0 = 0; f0 < n && s.rc == 0; f0 += per) {
-        const int64_t k = std::min<int64_t>(per, n - f0);
+    auto frames_of = [&](int64_t p) { return std::min<int64_t>(per, n - p * per); };
+    auto upload = [&](int64_t p) -> int {
+        const int k = (int)(p & 1);
+        if (p >= 2 && hipStreamWaitEvent(sup, kern_done[k], 0) != hipSuccess) return report(TMFWM_ERR_HIP, "stream wait failed");
+        if (int rc = up(s.start + p * per, frames_of(p), din[k], per * in_bytes, sup)) return rc;
+        return hipEventRecord(up_done[k], sup) == hipSuccess ? 0 : report(TMFWM_ERR_HIP, "event record failed");
+    };
+    auto download = [&](int64_t p) -> int {
+        const int k = (int)(p & 1);
+        if (hipStreamWaitEvent(sdown, kern_done[k], 0) != hipSuccess) return report(TMFWM_ERR_HIP, "stream wait failed");
+        if (int rc = down(s.start + p * per, frames_of(p), dout[k], sdown)) return rc;
+        return hipEventRecord(down_done[k], sdown) == hipSuccess ? 0 : report(TMFWM_ERR_HIP, "event record failed");
+    };
+    int rc = upload(0);
+    for (int64_t p = 0; p < npass && rc == 0; ++p) {
+        const int k = (int)(p & 1);
+        if (hipStreamWaitEvent(s.st, up_done[k], 0) != hipSuccess ||
+            (p >= 2 && hipStreamWaitEvent(s.st, down_done[k], 0) != hipSuccess)) {
+            rc = report(TMFWM_ERR_HIP, "stream wait failed");
+            break;
+        }
+        rc = kern(frames_of(p), din[k], per * in_bytes, dout[k], s.st, sink + 3 * chunks_per_pass * p);
+        if (rc == 0 && hipEventRecord(kern_done[k], s.st) != hipSuccess) rc = report(TMFWM_ERR_HIP, "event record failed");
+        if (rc == 0 && p >= 1) rc = download(p - 1);
+        if (rc == 0 && p + 1 < npass) rc = upload(p + 1);
+    }
+    if (rc == 0) rc = download(npass - 1);
+    hipError_t se = hipSuccess;
+    for (hipStream_t x : {sup, s.st, sdown})
+        if (se == hipSuccess) se = hipStreamSynchronize(x);
+    if (rc == 0 && se != hipSuccess) rc = report(TMFWM_ERR_HIP, "shard stream failed: %s", hipGetErrorString(se));
+    for (int64_t p = 0; p < npass && rc == 0; ++p) {
         int64_t cnt = 0;
-        const int rc = body(s.start + f0, k, din, per * in_bytes, dout, s.st, &cnt);
-        if (rc) fail_here(rc, tmfwm_last_error());
+        rc = tmf::sum_sink(sink + 3 * chunks_per_pass * p, tmf::count_chunks(frames_of(p), H, W, block), &cnt);
         s.lapack += cnt;
     }
-    if (s.rc == 0 && hipStreamSynchronize(s.st) != hipSuccess) fail_here(TMFWM_ERR_HIP, "shard stream failed");
-    (void)hipFree(din);
-    (void)hipFree(dout);
+    if (rc) fail_here(rc, tmfwm_last_error());
+    cleanup();
 }
 
 int join(std::vector<Shard> &sh, std::vector<std::thread> &th, int64_t *n_lapack)
@@ -316,20 +428,31 @@ int tmfwm_embed_multi(const uint8_t *rgb, int64_t n_frames, int32_t height, int3
         const DeviceTile *up = &uniq[shard.unique];
         th.emplace_back([=] {
             const DeviceTile &u = *up;
-            run_shard(*sp, u, fbytes, fbytes, 1,
-                      [&](int64_t f, int64_t k, uint8_t *din, int64_t, uint8_t *dout, hipStream_t st, int64_t *cnt) -> int {
-                          for (int64_t i = 0; i < k; ++i)
-                              if (hipMemcpyAsync(din + i * fbytes, rgb + (f + i) * frame_stride, (size_t)fbytes, hipMemcpyHostToDevice,
-                                                 st) != hipSuccess)
-                                  return report(TMFWM_ERR_HIP, "frame upload failed");
-                          int rc = tmfwm_embed_ex(din, k, height, width, fbytes, u.tile, block, alpha, dout, TMFWM_MEM_DEVICE, st, cnt);
-                          if (rc) return rc;
-                          for (int64_t i = 0; i < k; ++i)
-                              if (hipMemcpyAsync(out + (f + i) * frame_stride, dout + i * fbytes, (size_t)fbytes, hipMemcpyDeviceToHost,
-                                                 st) != hipSuccess)
-                                  return report(TMFWM_ERR_HIP, "frame download failed");
-                          return hipStreamSynchronize(st) == hipSuccess ? 0 : report(TMFWM_ERR_HIP, "shard stream failed");
-                      });
+            run_shard(
+                *sp, u, fbytes, fbytes, 1, height, width, block,
+                [&](int64_t f, int64_t k, uint8_t *din, int64_t, hipStream_t st) -> int {
+                    if (frame_stride == fbytes)
+                        return hipMemcpyAsync(din, rgb + f * frame_stride, (size_t)(k * fbytes), hipMemcpyHostToDevice, st) == hipSuccess
+                                   ? 0 : report(TMFWM_ERR_HIP, "frame upload failed");
+                    for (int64_t i = 0; i < k; ++i)
+                        if (hipMemcpyAsync(din + i * fbytes, rgb + (f + i) * frame_stride, (size_t)fbytes, hipMemcpyHostToDevice, st) !=
+                            hipSuccess)
+                            return report(TMFWM_ERR_HIP, "frame upload failed");
+                    return 0;
+                },
+                [&](int64_t k, const uint8_t *din, int64_t, uint8_t *dout, hipStream_t st, uint32_t *sink) -> int {
+                    return tmf::embed_device_async(din, k, height, width, fbytes, u.tile, block, alpha, dout, st, sink);
+                },
+                [&](int64_t f, int64_t k, const uint8_t *dout, hipStream_t st) -> int {
+                    if (frame_stride == fbytes)
+                        return hipMemcpyAsync(out + f * frame_stride, dout, (size_t)(k * fbytes), hipMemcpyDeviceToHost, st) == hipSuccess
+                                   ? 0 : report(TMFWM_ERR_HIP, "frame download failed");
+                    for (int64_t i = 0; i < k; ++i)
+                        if (hipMemcpyAsync(out + (f + i) * frame_stride, dout + i * fbytes, (size_t)fbytes, hipMemcpyDeviceToHost, st) !=
+                            hipSuccess)
+                            return report(TMFWM_ERR_HIP, "frame download failed");
+                    return 0;
+                });
         });
     }
     return join(sh, th, n_lapack_blocks);
@@ -358,21 +481,24 @@ int tmfwm_extract_multi(const uint8_t *wm_rgb, const uint8_t *orig_rgb, int64_t 
         Shard *sp = &shard;
         const DeviceTile *up = &uniq[shard.unique];
         th.emplace_back([=] {
-            run_shard(*sp, *up, fbytes, tbytes, 2,
-                      [&](int64_t f, int64_t k, uint8_t *din, int64_t half, uint8_t *dout, hipStream_t st, int64_t *cnt) -> int {
-                          for (int64_t i = 0; i < k; ++i) {
-                              if (hipMemcpyAsync(din + i * fbytes, wm_rgb + (f + i) * frame_stride, (size_t)fbytes,
-                                                 hipMemcpyHostToDevice, st) != hipSuccess ||
-                                  hipMemcpyAsync(din + half + i * fbytes, orig_rgb + (f + i) * frame_stride, (size_t)fbytes,
-                                                 hipMemcpyHostToDevice, st) != hipSuccess)
-                                  return report(TMFWM_ERR_HIP, "frame upload failed");
-                          }
-                          int rc = tmfwm_extract_ex(din, din + half, k, height, width, fbytes, block, alpha, dout, TMFWM_MEM_DEVICE, st, cnt);
-                          if (rc) return rc;
-                          if (hipMemcpyAsync(out_tiles + f * tbytes, dout, (size_t)(k * tbytes), hipMemcpyDeviceToHost, st) != hipSuccess)
-                              return report(TMFWM_ERR_HIP, "tile download failed");
-                          return hipStreamSynchronize(st) == hipSuccess ? 0 : report(TMFWM_ERR_HIP, "shard stream failed");
-                      });
+            run_shard(
+                *sp, *up, fbytes, tbytes, 2, height, width, block,
+                [&](int64_t f, int64_t k, uint8_t *din, int64_t half, hipStream_t st) -> int {
+                    for (int64_t i = 0; i < k; ++i)
+                        if (hipMemcpyAsync(din + i * fbytes, wm_rgb + (f + i) * frame_stride, (size_t)fbytes, hipMemcpyHostToDevice, st) !=
+                                hipSuccess ||
+                            hipMemcpyAsync(din + half + i * fbytes, orig_rgb + (f + i) * frame_stride, (size_t)fbytes,
+                                           hipMemcpyHostToDevice, st) != hipSuccess)
+                            return report(TMFWM_ERR_HIP, "frame upload failed");
+                    return 0;
+                },
+                [&](int64_t k, const uint8_t *din, int64_t half, uint8_t *dout, hipStream_t st, uint32_t *sink) -> int {
+                    return tmf::extract_device_async(din, din + half, k, height, width, fbytes, block, alpha, dout, st, sink);
+                },
+                [&](int64_t f, int64_t k, const uint8_t *dout, hipStream_t st) -> int {
+                    return hipMemcpyAsync(out_tiles + f * tbytes, dout, (size_t)(k * tbytes), hipMemcpyDeviceToHost, st) == hipSuccess
+                               ? 0 : report(TMFWM_ERR_HIP, "tile download failed");
+                });
         });
     }
     return join(sh, th, n_lapack_blocks);

@@ -28,7 +28,7 @@ from typing import Callable, Iterable, Sequence
 import numpy as np
 from PIL import Image
 
-from .constants import ALPHA, BLOCK_SIZE
+from .constants import ALPHA, BLOCK_SIZE, SVD_ROUTE
 
 
 @dataclass
@@ -61,13 +61,14 @@ class GpuStage:
     Returns (pixels, wait) where ``wait()`` blocks until the D2H copy landed.  The
     tile for an image size is prepared on the device once and reused."""
 
-    def __init__(self, watermark_data, block: int, alpha: float, preserve_ratio: bool, device=None):
+    def __init__(self, watermark_data, block: int, alpha: float, preserve_ratio: bool, device=None, route: str = SVD_ROUTE):
         import torch
 
         from . import batch
 
         self.torch, self.batch = torch, batch
         self.block, self.alpha, self.preserve_ratio = int(block), float(alpha), bool(preserve_ratio)
+        self.route = route  # the drop-in's SVD route (constants.SVD_ROUTE, custom_settings["svd_route"])
         self.device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
         wm = watermark_data if isinstance(watermark_data, Image.Image) else Image.open(io.BytesIO(watermark_data))
         grey = np.array(wm.convert("L"), dtype=np.uint8, copy=True)  # watermarking.py:98-103
@@ -94,7 +95,7 @@ class GpuStage:
         tile = self._tile(nbh, nbw)
         with torch.cuda.stream(self.stream):
             dev_in = host_in.to(self.device, non_blocking=True)
-            dev_out = self.batch.embed_batch(dev_in, tile, self.block, self.alpha, stream=self.stream)
+            dev_out = self.batch.embed_batch(dev_in, tile, self.block, self.alpha, stream=self.stream, route=self.route)
             host_out.copy_(dev_out, non_blocking=True)
             done = torch.cuda.Event()
             done.record(self.stream)
@@ -115,7 +116,8 @@ def embed_images(images: Iterable, watermark_data, preserve_ratio: bool = True, 
     settings = custom_settings or {}
     block = int(settings.get("block_size", BLOCK_SIZE))
     alpha = float(settings.get("alpha", ALPHA))
-    stage = device_stage or GpuStage(watermark_data, block, alpha, preserve_ratio)
+    route = settings.get("svd_route") or os.environ.get("TMFWM_SVD_ROUTE") or SVD_ROUTE  # as watermarking._route
+    stage = device_stage or GpuStage(watermark_data, block, alpha, preserve_ratio, route=route)
     n_workers = workers or min(16, max(2, (len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else 4)))
     sources: Sequence = list(images)
     with ThreadPoolExecutor(n_workers, thread_name_prefix="tmf-io") as pool:

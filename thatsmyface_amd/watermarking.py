@@ -19,13 +19,16 @@ uint8 RGB(A) / float32 as the reference itself produces them.
 from __future__ import annotations
 
 import ctypes
+import hashlib
 import io
+import os
+import threading
 
 import numpy as np
 from PIL import Image
 
 from . import _lib
-from .constants import ALPHA, BLOCK_SIZE
+from .constants import ALPHA, BLOCK_SIZE, SVD_ROUTE
 
 __all__ = [
     "get_watermark_settings",
@@ -160,25 +163,74 @@ def _settings(custom_settings):
     return settings.get("block_size", BLOCK_SIZE), settings.get("alpha", ALPHA)
 
 
+def _route(custom_settings) -> int:
+    """The SVD route of one drop-in call: custom_settings["svd_route"] if given,
+    else the TMFWM_SVD_ROUTE environment variable, else constants.SVD_ROUTE.  "reference"
+    computes every block's SVD with np.linalg.svd's own arithmetic (the dgesdd route), so
+    the bytes are the reference's by construction; "hybrid" is the batch path's route."""
+    r = (custom_settings or {}).get("svd_route") if isinstance(custom_settings, dict) else None
+    return _lib.route_code(r or os.environ.get("TMFWM_SVD_ROUTE") or SVD_ROUTE)
+
+
+def _rgb_image(img):
+    """img.convert("RGB") as the reference calls it (:154, :242-243), without its copy when the
+    image already is RGB (the pixels are only read)."""
+    return img if img.mode == "RGB" else img.convert("RGB")
+
+
+# Prepared watermark tiles of PNG-bytes watermarks, keyed by the bytes' digest and the tile
+# geometry: the app embeds one QR code into every uploaded image (embed_watermark_page.py:
+# 492-558), and its decode + resample would otherwise be redone per image (DESIGN.md 6).
+_TILE_CACHE_MAX = 16
+_tile_cache: "dict[tuple, np.ndarray]" = {}
+_tile_lock = threading.Lock()
+# Per-thread output staging of embed_watermark: Image.fromarray copies an RGB array into PIL's
+# own storage, so the array is reused by the thread's next call (no fresh pages to fault in).
+_tls = threading.local()
+
+
+def _tile_for(watermark_data, nbh, nbw, preserve_ratio) -> np.ndarray:
+    if not isinstance(watermark_data, bytes):
+        return np.ascontiguousarray(np.asarray(resize_watermark(watermark_data, nbh, nbw, preserve_ratio), dtype=np.uint8))
+    key = (hashlib.sha256(watermark_data).digest(), nbh, nbw, bool(preserve_ratio))
+    with _tile_lock:
+        t = _tile_cache.get(key)
+    if t is None:
+        t = np.ascontiguousarray(np.asarray(resize_watermark(Image.open(io.BytesIO(watermark_data)), nbh, nbw, preserve_ratio),
+                                            dtype=np.uint8))
+        t.setflags(write=False)
+        with _tile_lock:
+            if len(_tile_cache) >= _TILE_CACHE_MAX:
+                _tile_cache.pop(next(iter(_tile_cache)))
+            _tile_cache[key] = t
+    return t
+
+
 def embed_watermark(image, watermark_data, preserve_ratio=False, custom_settings=None):
     """watermarking.py:135-221: returns a new RGB PIL image of the same size."""
     block_size, alpha = _settings(custom_settings)
-    image = image.convert("RGB")
-    watermark_img = Image.open(io.BytesIO(watermark_data)) if isinstance(watermark_data, bytes) else watermark_data
+    image = _rgb_image(image)
     rgb = np.ascontiguousarray(np.asarray(image, dtype=np.uint8))
     height, width = rgb.shape[:2]
     block_size = int(block_size)
     if block_size <= 0:
         raise ValueError(f"block_size must be positive, got {block_size}")
     nbh, nbw = height // block_size, width // block_size
-    tile = np.ascontiguousarray(np.asarray(resize_watermark(watermark_img, nbh, nbw, preserve_ratio), dtype=np.uint8))
-    out = np.empty_like(rgb)
+    tile = _tile_for(watermark_data, nbh, nbw, preserve_ratio)
+    out = getattr(_tls, "out", None)
+    if out is None or out.shape != rgb.shape:
+        out = np.empty_like(rgb)
+    _tls.out = None  # owned by this call until PIL has copied it
     L = _lib.load()
     _lib.check(
-        L.tmfwm_embed(_ptr(rgb), 1, height, width, rgb.size, _ptr(tile), block_size, float(alpha), _ptr(out), _lib.MEM_HOST, None),
+        L.tmfwm_embed_route(_ptr(rgb), 1, height, width, rgb.size, _ptr(tile), block_size, float(alpha), _ptr(out), _lib.MEM_HOST,
+                            None, _route(custom_settings), None),
         "embed_watermark",
     )
-    return Image.fromarray(out)
+    img = Image.fromarray(out)
+    if not getattr(img, "readonly", 0):  # PIL copied the pixels: the array is free again
+        _tls.out = out
+    return img
 
 
 def extract_watermark(watermarked_image, original_image, custom_settings=None):
@@ -187,8 +239,8 @@ def extract_watermark(watermarked_image, original_image, custom_settings=None):
     block_size = int(block_size)
     if block_size <= 0:
         raise ValueError(f"block_size must be positive, got {block_size}")
-    w = np.asarray(watermarked_image.convert("RGB"), dtype=np.uint8)
-    o = np.asarray(original_image.convert("RGB"), dtype=np.uint8)
+    w = np.asarray(_rgb_image(watermarked_image), dtype=np.uint8)
+    o = np.asarray(_rgb_image(original_image), dtype=np.uint8)
     height, width = w.shape[:2]
     nbh, nbw = height // block_size, width // block_size
     if nbh == 0 or nbw == 0:
@@ -202,7 +254,8 @@ def extract_watermark(watermarked_image, original_image, custom_settings=None):
     out = np.empty((nbh, nbw), np.uint8)
     L = _lib.load()
     _lib.check(
-        L.tmfwm_extract(_ptr(w), _ptr(o), 1, height, width, w.size, block_size, float(alpha), _ptr(out), _lib.MEM_HOST, None),
+        L.tmfwm_extract_route(_ptr(w), _ptr(o), 1, height, width, w.size, block_size, float(alpha), _ptr(out), _lib.MEM_HOST,
+                              None, _route(custom_settings), None),
         "extract_watermark",
     )
     return Image.fromarray(out)

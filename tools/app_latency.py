@@ -55,6 +55,9 @@ def main():
     wm_img = W.embed_watermark(cover, png, True, cs)
     out["embed_watermark_ms"] = timed(lambda: W.embed_watermark(cover, png, True, cs))
     out["extract_watermark_ms"] = timed(lambda: W.extract_watermark(wm_img, cover, cs))
+    rs = dict(cs, svd_route="reference")
+    out["embed_watermark_reference_route_ms"] = timed(lambda: W.embed_watermark(cover, png, True, rs))
+    out["extract_watermark_reference_route_ms"] = timed(lambda: W.extract_watermark(wm_img, cover, rs))
     # where embed_watermark's time goes (its stages, each timed alone)
     from thatsmyface_amd import _lib
     rgb = np.ascontiguousarray(np.asarray(cover.convert("RGB"), dtype=np.uint8))

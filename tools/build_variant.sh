@@ -8,15 +8,22 @@
 # SRC_SED='<sed script>' compiles the kernel TUs from a copy of the sources edited by that
 # script (e.g. SRC_SED='s/kPowerIters = 6/kPowerIters = 4/'): experiments without switches
 # in the product code.  SRC_REV=<git revision> compiles the kernel TUs of that revision
-# instead (e.g. the build before a change, for an A/B on one box).
+# instead (e.g. the build before a change, for an A/B on one box).  SRC_DIR=<dir> compiles the
+# kernel TUs from a copy of the csrc tree kept elsewhere (e.g. a git worktree with an
+# experimental edit).  NOMAKE=1 skips the main build's make (its objects are linked as they are).
 set -euo pipefail
 NAME=$1; shift
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 C=$ROOT/thatsmyface_amd/csrc
-make -s -C "$C" >/dev/null
+[ "${NOMAKE:-0}" = "1" ] || make -s -C "$C" >/dev/null
 T=$(mktemp -d)
 K=$C
-if [ -n "${SRC_REV:-}" ]; then
+if [ -n "${SRC_DIR:-}" ]; then
+  K=$T/thatsmyface_amd/csrc
+  mkdir -p "$K" "$T/include"
+  cp "$SRC_DIR"/thatsmyface_amd/csrc/*.h "$SRC_DIR"/thatsmyface_amd/csrc/*.hip "$K"/
+  cp "$SRC_DIR"/include/*.h "$T/include/"
+elif [ -n "${SRC_REV:-}" ]; then
   git -C "$ROOT" archive "$SRC_REV" thatsmyface_amd/csrc include | tar -x -C "$T"
   K=$T/thatsmyface_amd/csrc
 elif [ -n "${SRC_SED:-}" ]; then

@@ -1,0 +1,12 @@
+# round-4 A/B: reconstruction chain loop order (embed spills) and dgesdd-route fixup occupancy
+set -euo pipefail
+TAG=${TAG:-r04b}
+O=gpurun_out/$TAG
+mkdir -p $O
+timeout -k 10 300 python -u tools/ab_variants.py --block 16 --frames 64 --rounds 3 base chain both > $O/ab_b16.log 2>&1
+timeout -k 10 300 python -u tools/ab_variants.py --block 8 --frames 128 --rounds 3 base chain both > $O/ab_b8.log 2>&1
+timeout -k 10 200 python -u tools/ab_variants.py --block 12 --frames 64 --rounds 2 base chain > $O/ab_b12.log 2>&1
+timeout -k 10 200 python -u tools/ab_variants.py --block 16 --frames 32 --rounds 2 --cover photo base chain > $O/ab_b16_photo.log 2>&1
+timeout -k 10 300 python -u tools/exp/ref_route_time.py --block 8 --frames 16 --rounds 2 base fx4 fx6 fx8 > $O/ref_route_b8.log 2>&1
+timeout -k 10 300 python -u tools/exp/ref_route_time.py --block 16 --frames 8 --rounds 2 base fx4 fx8 > $O/ref_route_b16.log 2>&1
+echo done
