@@ -334,18 +334,24 @@ TMF_DEVI void embed_blocks(const EmbedArgs &a, const StripPos &pos, uint32_t id,
             if (real_row<B>(q, r)) tile[rk[k] * LD + q * R + r] = sk * Vf[r][k];
     }
     __syncthreads();
+    // k outermost: each element of Bm is read from LDS once and used by this lane's R rows at
+    // once.  Row by row, the compiler hoisted all b^2 reads across the rows and spilled them:
+    // 40 of embed<16>'s 47 spilled VGPRs (scratch traffic ~1x the frame's bytes); this order
+    // keeps 7 (A/B on one box, identical hashes: embed<16> -0.9 % noise / -1.7 % camera-like
+    // covers, embed<8> / <12> +-0, profiles/r04/r04b/ab_*.log).  Every M[r][j] is the same fma
+    // chain over k = 0..b-1.
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-        float m[B];
+    for (int r = 0; r < R; ++r)
 #pragma unroll
-        for (int j = 0; j < B; ++j) m[j] = 0.0f;
+        for (int j = 0; j < B; ++j) x[r][j] = 0.0f;
 #pragma unroll
-        for (int k = 0; k < B; ++k)
+    for (int k = 0; k < B; ++k)
 #pragma unroll
-            for (int j = 0; j < B; ++j) m[j] = __builtin_fmaf(Us[r][k], tile[k * LD + j], m[j]);
+        for (int j = 0; j < B; ++j) {
+            const float bkj = tile[k * LD + j];
 #pragma unroll
-        for (int j = 0; j < B; ++j) x[r][j] = m[j];
-    }
+            for (int r = 0; r < R; ++r) x[r][j] = __builtin_fmaf(Us[r][k], bkj, x[r][j]);
+        }
     __syncthreads();
     stamp(4);
     dct2d_rows_layout<B, true>(x, tile, q);  // :204

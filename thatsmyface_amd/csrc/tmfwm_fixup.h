@@ -10,12 +10,14 @@
 // image; extract_fixup_kernel<b> computes both sigma_1 on the dgesdd route and writes the
 // byte.
 //
-// One 64-lane workgroup (one wave) per listed block, its working set in LDS: the pixel,
-// colour and transform work is spread over the lanes (a pixel, a DCT row or column, an
-// element of the reconstruction per lane), and the dgesdd route runs under
-// lp::WavePar (its matrix loops over the lanes, its scalar recurrences on every lane
-// alike).  A grid-stride loop over the device-side count: no host round trip sits between
-// the passes, and a short list costs one block's latency, not one serial dgesdd per thread.
+// A group of G = 8 (b <= 8) or 16 lanes per listed block, 64 / G blocks per wave, each group's
+// working set in LDS: the pixel, colour and transform work is spread over the group's lanes
+// (a pixel, a DCT row or column, an element of the reconstruction per lane), and the dgesdd
+// route runs under lp::GroupPar<G> (its matrix loops over the group's lanes, its scalar
+// recurrences on the group's lanes alike).  A grid-stride loop over the device-side count: no
+// host round trip sits between the passes.  (Until round 4 one 64-lane wave took one block,
+// lp::WavePar; with every block of the reference route coming here, the scalar recurrences
+// left the SIMDs idle -- DESIGN.md 3.5.)
 // dbdsqr's non-convergence (np.linalg.svd raises LinAlgError there) is counted in *fb_bad.
 #pragma once
 #include "tmfwm_device.h"
@@ -37,40 +39,54 @@ TMF_DEVI int runtime_n(int n)
     return n;
 }
 
-// this block's luma, then its 2-D DCT (axis 0, then axis 1: watermarking.py:192, :279-282),
-// into t[B*B] (row-major) -- lanes take pixels, then columns, then rows
+// Lanes per listed block (lp::GroupPar<G>): 64 / G blocks per wave.  Round 4: the reference
+// route (TMFWM_ROUTE_REFERENCE) sends every block here, so the pass is a throughput path, not
+// a few stragglers' latency: one block per wave left the SIMDs idle on the route's scalar
+// recurrences.
 template <int B>
-TMF_DEVI void fix_load_dct(const uint8_t *frame, int W, int bi, int bj, float *t, int lane)
+constexpr int kFixLanes = B <= 8 ? 8 : 16;
+
+// a group's lanes see each other's LDS writes in program order (one wave): only the compiler
+// must not move LDS accesses across the phase boundaries
+TMF_DEVI void group_sync() { asm volatile("" ::: "memory"); }
+
+// this block's luma, then its 2-D DCT (axis 0, then axis 1: watermarking.py:192, :279-282),
+// into t[B*B] (row-major) -- the group's lanes take pixels, then columns, then rows
+template <int B, int G>
+TMF_DEVI void fix_load_dct(const uint8_t *frame, int W, int bi, int bj, float *t, int gl)
 {
-    for (int k = lane; k < B * B; k += 64) {
+    for (int k = gl; k < B * B; k += G) {
         const uint8_t *p = frame + ((int64_t)(bi * B + k / B) * W + (int64_t)bj * B + k % B) * 3;
         t[k] = luma(p[0], p[1], p[2]);
     }
-    __syncthreads();
-    if (lane < B) {
+    group_sync();
+    for (int c = gl; c < B; c += G) {
         float col[B];
 #pragma unroll
-        for (int r = 0; r < B; ++r) col[r] = t[r * B + lane];
+        for (int r = 0; r < B; ++r) col[r] = t[r * B + c];
         dct::dct2<B>(col);
 #pragma unroll
-        for (int r = 0; r < B; ++r) t[r * B + lane] = col[r];
+        for (int r = 0; r < B; ++r) t[r * B + c] = col[r];
     }
-    __syncthreads();
-    if (lane < B) {
+    group_sync();
+    for (int r = gl; r < B; r += G) {
         float row[B];
 #pragma unroll
-        for (int c = 0; c < B; ++c) row[c] = t[lane * B + c];
+        for (int c = 0; c < B; ++c) row[c] = t[r * B + c];
         dct::dct2<B>(row);
 #pragma unroll
-        for (int c = 0; c < B; ++c) t[lane * B + c] = row[c];
+        for (int c = 0; c < B; ++c) t[r * B + c] = row[c];
     }
-    __syncthreads();
+    group_sync();
 }
 
+// one group's LDS: the route's workspace (its U and VT, f64 column-major at ws + B^2 and
+// ws + 2 B^2, are read in place by the reconstruction), the DCT block D -- dead once the route
+// has copied it, so the reconstruction M reuses it -- and S
 template <int B>
 struct FixLds {
     double ws[lp::ws_doubles(B)];
-    float D[B * B], U[B * B], Vt[B * B], S[B], M[B * B];
+    float D[B * B], S[B];
 };
 
 TMF_DEVI void block_of(uint32_t id, uint32_t per_frame, int nbw, int64_t &fr, int &bi, int &bj)
@@ -84,61 +100,71 @@ TMF_DEVI void block_of(uint32_t id, uint32_t per_frame, int nbw, int64_t &fr, in
 template <int B>
 __global__ __launch_bounds__(64) void embed_fixup_kernel(EmbedArgs a, const uint32_t *__restrict__ list, const uint32_t *__restrict__ count)
 {
-    __shared__ FixLds<B> f;
-    const int lane = (int)threadIdx.x;
+    constexpr int G = kFixLanes<B>, NG = 64 / G;
+    static_assert(G >= B, "a group holds one element of dbdsqr's vectors per lane");
+    using Par = lp::GroupPar<G>;
+    __shared__ FixLds<B> fl[NG];
+    const int gl = Par::lane(), grp = (int)(threadIdx.x / G);
+    FixLds<B> &f = fl[grp];
     const uint32_t n = *count;
     const uint32_t per_frame = (uint32_t)a.nbh * (uint32_t)a.nbw;
-    for (uint32_t t = blockIdx.x; t < n; t += gridDim.x) {
+    for (uint32_t t0 = blockIdx.x * NG; t0 < n; t0 += gridDim.x * NG) {
+        const uint32_t t = t0 + (uint32_t)grp;
+        if (t >= n) continue;  // this group has no block in this round
         int64_t fr;
         int bi, bj;
         block_of(list[t], per_frame, a.nbw, fr, bi, bj);
         const uint8_t *src = a.src + fr * a.frame_stride;
         uint8_t *dst = a.dst + fr * a.frame_stride;
-        fix_load_dct<B>(src, a.W, bi, bj, f.D, lane);
-        const int info = lp::svd_f32_ws<true, lp::WavePar>(f.D, runtime_n(B), f.U, f.S, f.Vt, f.ws);  // :195
-        if (info && lane == 0 && a.fb_bad) atomicAdd(a.fb_bad, 1u);
-        // :198 blend, :201 U @ (diag(S) @ Vt) as OpenBLAS sgemm's fma chain over k
+        fix_load_dct<B, G>(src, a.W, bi, bj, f.D, gl);
+        const int info = lp::svd_f32_ws<true, Par>(f.D, runtime_n(B), nullptr, f.S, nullptr, f.ws);  // :195
+        if (info && gl == 0 && a.fb_bad) atomicAdd(a.fb_bad, 1u);
+        // :198 blend, :201 U @ (diag(S) @ Vt) as OpenBLAS sgemm's fma chain over k, on U and Vt
+        // rounded to f32 (numpy's astype) from the route's f64 U and VT
+        const double *U64 = f.ws + B * B, *VT64 = f.ws + 2 * B * B;
+        float *M = f.D;
         const double w = (double)a.wm[(int64_t)bi * a.nbw + bj];
         const float s0 = (float)((double)f.S[0] + a.alpha * (w / 255.0));
-        for (int e = lane; e < B * B; e += 64) {
+        for (int e = gl; e < B * B; e += G) {
             const int i = e / B, j = e % B;
             float acc = 0.0f;
 #pragma unroll
-            for (int k = 0; k < B; ++k) acc = __builtin_fmaf(f.U[i * B + k], (k == 0 ? s0 : f.S[k]) * f.Vt[k * B + j], acc);
-            f.M[e] = acc;
+            for (int k = 0; k < B; ++k)
+                acc = __builtin_fmaf((float)U64[i + k * B], (k == 0 ? s0 : f.S[k]) * (float)VT64[k + j * B], acc);
+            M[e] = acc;
         }
-        __syncthreads();
+        group_sync();
         // :204 IDCT, axis 0 then axis 1
-        if (lane < B) {
+        for (int c = gl; c < B; c += G) {
             float col[B];
 #pragma unroll
-            for (int r = 0; r < B; ++r) col[r] = f.M[r * B + lane];
+            for (int r = 0; r < B; ++r) col[r] = M[r * B + c];
             dct::dct3<B>(col);
 #pragma unroll
-            for (int r = 0; r < B; ++r) f.M[r * B + lane] = col[r];
+            for (int r = 0; r < B; ++r) M[r * B + c] = col[r];
         }
-        __syncthreads();
-        if (lane < B) {
+        group_sync();
+        for (int r = gl; r < B; r += G) {
             float row[B];
 #pragma unroll
-            for (int c = 0; c < B; ++c) row[c] = f.M[lane * B + c];
+            for (int c = 0; c < B; ++c) row[c] = M[r * B + c];
             dct::dct3<B>(row);
 #pragma unroll
-            for (int c = 0; c < B; ++c) f.M[lane * B + c] = row[c];
+            for (int c = 0; c < B; ++c) M[r * B + c] = row[c];
         }
-        __syncthreads();
+        group_sync();
         // :207-216 write back with the pixel's own chroma, inverse colour
-        for (int k = lane; k < B * B; k += 64) {
+        for (int k = gl; k < B * B; k += G) {
             const int64_t off = ((int64_t)(bi * B + k / B) * a.W + (int64_t)bj * B + k % B) * 3;
             float cbs, crs;
             chroma(src[off], src[off + 1], src[off + 2], cbs, crs);
             uint32_t R8, G8, B8;
-            colour_inv(f.M[k], cbs, crs, R8, G8, B8);
+            colour_inv(M[k], cbs, crs, R8, G8, B8);
             dst[off] = (uint8_t)R8;
             dst[off + 1] = (uint8_t)G8;
             dst[off + 2] = (uint8_t)B8;
         }
-        __syncthreads();  // the LDS slots are reused by the next listed block
+        group_sync();  // the group's LDS slots are reused by its next listed block
     }
 }
 
@@ -146,24 +172,30 @@ template <int B>
 __global__ __launch_bounds__(64) void extract_fixup_kernel(ExtractArgs a, const uint32_t *__restrict__ list,
                                                            const uint32_t *__restrict__ count)
 {
-    __shared__ FixLds<B> f;
-    const int lane = (int)threadIdx.x;
+    constexpr int G = kFixLanes<B>, NG = 64 / G;
+    static_assert(G >= B, "a group holds one element of dbdsqr's vectors per lane");
+    using Par = lp::GroupPar<G>;
+    __shared__ FixLds<B> fl[NG];
+    const int gl = Par::lane(), grp = (int)(threadIdx.x / G);
+    FixLds<B> &f = fl[grp];
     const uint32_t n = *count;
     const uint32_t per_frame = (uint32_t)a.nbh * (uint32_t)a.nbw;
-    for (uint32_t t = blockIdx.x; t < n; t += gridDim.x) {
+    for (uint32_t t0 = blockIdx.x * NG; t0 < n; t0 += gridDim.x * NG) {
+        const uint32_t t = t0 + (uint32_t)grp;
+        if (t >= n) continue;
         int64_t fr;
         int bi, bj;
         block_of(list[t], per_frame, a.nbw, fr, bi, bj);
         float sig[2];
         for (int img = 0; img < 2; ++img) {
-            fix_load_dct<B>((img == 0 ? a.wsrc : a.osrc) + fr * a.frame_stride, a.W, bi, bj, f.D, lane);
-            const int info = lp::svd_f32_ws<false, lp::WavePar>(f.D, runtime_n(B), nullptr, f.S, nullptr, f.ws);  // :279-282
-            if (info && lane == 0 && a.fb_bad) atomicAdd(a.fb_bad, 1u);
+            fix_load_dct<B, G>((img == 0 ? a.wsrc : a.osrc) + fr * a.frame_stride, a.W, bi, bj, f.D, gl);
+            const int info = lp::svd_f32_ws<false, Par>(f.D, runtime_n(B), nullptr, f.S, nullptr, f.ws);  // :279-282
+            if (info && gl == 0 && a.fb_bad) atomicAdd(a.fb_bad, 1u);
             sig[img] = f.S[0];
-            __syncthreads();
+            group_sync();
         }
         // :285-289 (numpy-2 NEP 50): f32 difference / f32(alpha); clip and *255 in f64; truncate
-        if (lane == 0) {
+        if (gl == 0) {
             const float e = (sig[0] - sig[1]) / a.alpha32;
             double d = (double)e;
             d = d < 0.0 ? 0.0 : d;
@@ -178,22 +210,24 @@ __global__ __launch_bounds__(64) void extract_fixup_kernel(ExtractArgs a, const 
 // possible list length); workgroups past the device-side count exit at once, the others
 // stride over it
 // ---------------------------------------------------------------------------
+template <int B>
 inline unsigned fixup_grid(int64_t entries)
 {
-    return (unsigned)(entries < 1 ? 1 : (entries > 8192 ? 8192 : entries));
+    const int64_t waves = (entries + 64 / kFixLanes<B> - 1) / (64 / kFixLanes<B>);
+    return (unsigned)(waves < 1 ? 1 : (waves > 8192 ? 8192 : waves));
 }
 
 template <int B>
 inline hipError_t embed_fixup_b(const EmbedArgs &a, const uint32_t *list, const uint32_t *count, int64_t max_entries, hipStream_t st)
 {
-    hipLaunchKernelGGL((embed_fixup_kernel<B>), dim3(fixup_grid(max_entries)), dim3(64), 0, st, a, list, count);
+    hipLaunchKernelGGL((embed_fixup_kernel<B>), dim3(fixup_grid<B>(max_entries)), dim3(64), 0, st, a, list, count);
     return hipGetLastError();
 }
 
 template <int B>
 inline hipError_t extract_fixup_b(const ExtractArgs &a, const uint32_t *list, const uint32_t *count, int64_t max_entries, hipStream_t st)
 {
-    hipLaunchKernelGGL((extract_fixup_kernel<B>), dim3(fixup_grid(max_entries)), dim3(64), 0, st, a, list, count);
+    hipLaunchKernelGGL((extract_fixup_kernel<B>), dim3(fixup_grid<B>(max_entries)), dim3(64), 0, st, a, list, count);
     return hipGetLastError();
 }
 

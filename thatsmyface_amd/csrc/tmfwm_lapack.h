@@ -69,6 +69,20 @@ struct WavePar {  // device code only
     static constexpr int kLanes = 64;
     __device__ __forceinline__ static void sync() { __syncthreads(); }  // workgroup == one wave
 };
+// G lanes per block, 64 / G blocks per wave (device code only): every group of G consecutive
+// lanes runs the route for its own block, the element loops over the group's lanes and the
+// scalar recurrences on each group's lanes alike, so the groups of a wave diverge only where
+// their blocks' data do (dbdsqr's iteration counts, splits and shifts).  A group's lanes see
+// each other's LDS writes in program order (one wave), so sync() only fences the compiler.
+template <int G>
+struct GroupPar {
+    static_assert(G == 8 || G == 16 || G == 32, "group size");
+    __device__ __forceinline__ static int lane() { return (int)(threadIdx.x & (unsigned)(G - 1)); }
+    __device__ __forceinline__ static int base() { return (int)(threadIdx.x & ~(unsigned)(G - 1) & 63u); }
+    static constexpr int kLanes = G;
+    __device__ __forceinline__ static void sync() { asm volatile("" ::: "memory"); }
+};
+
 template <class P, class = void>
 struct IsReverse { static constexpr bool v = false; };
 template <class P>
@@ -112,6 +126,30 @@ struct LVec<WavePar> {
     __device__ __forceinline__ void store_f32(float *dst, int n) const
     {
         if (WavePar::lane() < n) dst[WavePar::lane()] = (float)v;
+    }
+};
+
+// Under GroupPar<G> element i of a group's vector lives in the register of the group's lane i;
+// the index is uniform within the group but the lane differs between groups, so the read is a
+// ds_bpermute (per-lane source) rather than a readlane.
+template <int G>
+struct LVec<GroupPar<G>> {
+    double v = 0.0;
+    __device__ __forceinline__ double get(int i) const
+    {
+        const long long b = __builtin_bit_cast(long long, v);
+        const int addr = (GroupPar<G>::base() + i) << 2;
+        const int lo = __builtin_amdgcn_ds_bpermute(addr, (int)b), hi = __builtin_amdgcn_ds_bpermute(addr, (int)(b >> 32));
+        return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+    }
+    __device__ __forceinline__ void set(int i, double x) { v = GroupPar<G>::lane() == i ? x : v; }
+    __device__ __forceinline__ void load(const double *src, int n)
+    {
+        v = GroupPar<G>::lane() < n ? src[GroupPar<G>::lane()] : 0.0;
+    }
+    __device__ __forceinline__ void store_f32(float *dst, int n) const
+    {
+        if (GroupPar<G>::lane() < n) dst[GroupPar<G>::lane()] = (float)v;
     }
 };
 
@@ -980,10 +1018,12 @@ TMF_LPN int svd_f32_ws(const float *D, int n, float *Uo, float *So, float *Vto, 
     if (WANT_V) {
         apply_q<P>(n, A, tauq, U, work);
         apply_pt<P>(n, A, taup, VT, work);
-        LP_PAR(P, q, n * n) {
-            const int i = q / n, k = q - i * n;
-            Uo[i * n + k] = (float)U[i + k * n];
-            Vto[i * n + k] = (float)VT[i + k * n];
+        if (Uo) {  // NULL: the caller reads U (ws + n^2) and VT (ws + 2 n^2), column-major f64, itself
+            LP_PAR(P, q, n * n) {
+                const int i = q / n, k = q - i * n;
+                Uo[i * n + k] = (float)U[i + k * n];
+                Vto[i * n + k] = (float)VT[i + k * n];
+            }
         }
     }
     dv.store_f32(So, n);
