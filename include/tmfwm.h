@@ -148,7 +148,7 @@ int tmfwm_extract_route(const uint8_t *wm_rgb, const uint8_t *orig_rgb, int64_t 
  * result is back.  The n_frames frames are split into n_shards contiguous shards (sizes
  * differ by at most one, shard s gets frames [s*n/k + min(s, n%k), ...)), shard s runs on
  * HIP device devices[s] (devices = NULL: device s; n_shards <= 0 with devices = NULL: every
- * visible device) on its own host thread and stream, in passes of at most ~2 GiB of
+ * visible device) on its own host thread and streams, in passes through two device slots of ~1 GiB of
  * frames.  The watermark tile is uploaded to devices[0] and broadcast to every other
  * device of the set with RCCL (ncclBroadcast over xGMI; librccl.so.1 is loaded on first
  * use).  Shards naming the same device share its tile (logical shards).  Replaces the

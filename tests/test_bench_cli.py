@@ -108,6 +108,14 @@ def test_bench_eight_ranks_gloo(tmp_path):
     assert line["n_ranks"] == 8 and line["config"]["frames_total"] == 8 * F
     assert line["parity_sample"]["frames"] == 16 and line["parity_sample"]["embed_mismatch"] == 0
     assert line["lapack_route_sample"] == "8/8"
+    # self-contained N > 1 line: rank 0's CPU baseline on cores / N and the
+    # spread of the ranks' mean launch times
+    cb = line["cpu_baseline"]
+    assert cb and cb["kind"] == "port" and cb["value"] > 0 and cb["cores"] >= 1 and "rank 0's share" in cb["sample"]
+    lm = line["roofline"]["launch_ms_over_ranks"]
+    assert lm["ranks"] == 8 and 0 < lm["min"] <= line["roofline"]["launch_ms"] <= lm["max"]
+    xm = line["kernels_ms"]["extract_over_ranks"]
+    assert 0 < xm["min"] <= line["kernels_ms"]["extract"] <= xm["max"]
     frames = O.synth_bytes(0x5EED0001, 0, 8 * F, H * W * 3).reshape(8 * F, H, W, 3)
     tile = O.synth_bytes(0x5EED0002, 0, 1, (H // B) * (W // B)).reshape(H // B, W // B)
     ref = O.embed_batch(frames, tile, B, A, 1)

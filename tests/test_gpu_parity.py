@@ -85,6 +85,9 @@ def test_colour_helpers_non_uint8_gpu(dev):
     for dt in (np.float64, np.float32, np.float16):
         a = ycc.astype(dt)
         assert np.array_equal(W.ycbcr_to_rgb(a), O.ycbcr_to_rgb(a)), dt
+        # the same values in the other byte order: computed on the native layout
+        assert np.array_equal(W.ycbcr_to_rgb(a.astype(a.dtype.newbyteorder(">" if a.dtype.isnative else "<"))),
+                              O.ycbcr_to_rgb(a)), dt
 
 
 ALL_B = [4, 6, 8, 10, 12, 14, 16]  # the app's block-size slider (embed_watermark_page.py:324-331)
@@ -735,12 +738,17 @@ def test_multi_entry_points_logical_shards(dev, monkeypatch):
 
     from thatsmyface_amd import batch, multi
 
-    b, H, W, n = 8, 136, 200, 5
+    b, H, W, n = 8, 136, 200, 7
     host = np.stack([np.ascontiguousarray(cover(("noise", "smooth", "qr")[i % 3], H, W, 40 + i)) for i in range(n)])
     t = _u8(41, (H // b, W // b))
     ref_dev = batch.embed_batch(torch.from_numpy(host).to(dev), torch.from_numpy(t).to(dev), b, 0.1).cpu().numpy()
-    for shards, force in (([0, 0, 0], "0"), ([0], "1"), ([0, 0, 0, 0, 0, 0, 0], "1")):
+    one = H * W * 3
+    # the last case runs each shard in passes of 2 frames (2 x (in + out) per slot): both slots, the
+    # cross-pass waits and a short last pass
+    for shards, force, pass_bytes in (([0, 0, 0], "0", ""), ([0], "1", ""), ([0, 0, 0, 0, 0, 0, 0], "1", ""),
+                                      ([0], "0", str(4 * one)), ([0, 0], "0", str(4 * one))):
         monkeypatch.setenv("TMFWM_DEBUG_FORCE_RCCL", force)
+        monkeypatch.setenv("TMFWM_DEBUG_PASS_BYTES", pass_bytes)
         st, xs = {}, {}
         out = multi.embed_multi(host, t, b, 0.1, devices=shards, stats=st)
         assert np.array_equal(out, ref_dev), shards

@@ -120,7 +120,12 @@ struct DeviceTile {
 // that a pass's transfers overlap the neighbouring pass's kernels.
 int64_t pass_frames(int64_t frame_bytes)
 {
-    const int64_t budget = int64_t(1) << 30;
+    int64_t budget = int64_t(1) << 30;
+    // TMFWM_DEBUG_PASS_BYTES lowers the slot size so that the tests run several passes
+    if (const char *e = std::getenv("TMFWM_DEBUG_PASS_BYTES"); e && *e) {
+        const long long v = std::atoll(e);
+        if (v > 0 && v < budget) budget = (int64_t)v;
+    }
     const int64_t f = frame_bytes > 0 ? budget / frame_bytes : 1;
     return f < 1 ? 1 : f;
 }
