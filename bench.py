@@ -62,6 +62,10 @@ def parse(argv=None):
     p.add_argument("--lapack-frames", type=int, default=8,
                    help="frames of the parity sample also checked against the reference's own SVD arithmetic "
                         "(the oracle's dgesdd route, ~1 s per 4K frame per 16 cores; 0 = skip)")
+    p.add_argument("--exact-frames", type=int, default=64,
+                   help="hybrid route only: frames of the batch re-run on the GPU's reference route (the dgesdd "
+                        "route for every block, exact by construction) after the timed region, timed and "
+                        "compared byte for byte with the timed run's output (0 = skip)")
     p.add_argument("--pg-timeout", type=float, default=600.0,
                    help="seconds a rank may wait in a collective before the run fails (N > 1)")
     p.add_argument("--route", default="hybrid", choices=["hybrid", "reference"],
@@ -160,7 +164,40 @@ def gpu_kernels(route="hybrid"):
         embed_stats=lambda f, t, b, a, o: (lambda st: (batch.embed_batch(f, t, b, a, out=o, stats=st, route=route), st)[1])({}),
         embed_list_pass=lambda b: batch.embed_list_pass(b) and route == "hybrid",
         route=route,
+        exact_embed=lambda f, t, b, a, o: batch.embed_batch(f, t, b, a, out=o, route="reference"),
+        exact_extract=lambda w_, o_, b, a, out: batch.extract_batch(w_, o_, b, a, out=out, route="reference"),
     )
+
+
+def exact_route_sample(K, frames, tile, out, tiles, block, alpha, n, on_gpu):
+    """The hybrid route's bytes against the reference route's on the first n frames of the
+    timed batch, both on the GPU: the reference route runs the dgesdd route on
+    every block, np.linalg.svd's arithmetic by construction, so this counts the bytes where the
+    throughput route's statistical exactness failed, over far more blocks than the CPU oracle
+    can check.  Also times the reference route (embed + extract of its own output)."""
+    import torch
+
+    n = min(n, frames.shape[0])
+    if n <= 0 or not hasattr(K, "exact_embed"):
+        return None
+    f = frames[:n]
+    eo, et = torch.empty_like(f), torch.empty_like(tiles[:n])
+    K.exact_embed(f, tile, block, alpha, eo)  # warm: first call sizes the pools
+    sync = torch.cuda.synchronize if on_gpu else (lambda: None)
+    sync()
+    t0 = time.perf_counter()
+    K.exact_embed(f, tile, block, alpha, eo)
+    K.exact_extract(eo, f, block, alpha, et)
+    sync()
+    dt = time.perf_counter() - t0
+    H, W = f.shape[1], f.shape[2]
+    diff_e = int((eo != out[:n]).sum())
+    diff_x = int((et != tiles[:n]).sum())
+    return {"frames": n, "blocks": n * (H // block) * (W // block),
+            "embed_bytes_differing": diff_e, "extract_bytes_differing": diff_x,
+            "reference_route_Mpx_per_s": round(n * H * W / dt / 1e6, 1),
+            "what": "the timed (hybrid-route) output vs the GPU reference route (dgesdd route on every block) "
+                    "on the batch's first frames; reference-route rate = embed + extract of those frames"}
 
 
 def oracle_check(host_frames, host_tile, out, tiles, block, alpha, threads):
@@ -333,6 +370,9 @@ def run(args, kernels=None, device=None):
 
     rt = ShardedRoundTrip(embed_fn=K.embed, extract_fn=K.extract, frames=frames, tile=wm, block=b, alpha=alpha)
 
+    # the timing hooks run in the warmup steps too, so the timed steps pay no first-use cost
+    # (the first event records of a process take milliseconds on the host)
+    rt.hooks.append(hook)
     for _ in range(args.warmup):
         rt.step()
     # how one embed call over this rank's whole batch splits its work (untimed; the same bytes
@@ -348,7 +388,7 @@ def run(args, kernels=None, device=None):
     if world > 1:
         dist.barrier()
     sync()
-    rt.hooks.append(hook)
+    marks.clear()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         rt.step()
@@ -378,6 +418,10 @@ def run(args, kernels=None, device=None):
     extract_bytes = F * (6 * H * W + nbh * nbw)
     achieved = embed_bytes / (embed_ms * 1e-3) / 1e9
     achieved_read = F * embed_read / (embed_ms * 1e-3) / 1e9
+
+    exact = None
+    if rank == 0 and getattr(K, "route", "hybrid") == "hybrid" and args.exact_frames > 0:
+        exact = exact_route_sample(K, frames, wm, rt.out, rt.tiles, b, alpha, args.exact_frames, on_gpu)
 
     # parity of the timed batch against the oracle.  N = 1: rank 0 checks the CPU-baseline
     # sample (the batch's first --cpu-frames frames); N > 1: every rank checks its share of
@@ -556,6 +600,7 @@ def run(args, kernels=None, device=None):
             "parity_sample": parity,
             "lapack_route_sample": lapack_sample["summary"] if lapack_sample else None,
             "lapack_route_detail": lapack_sample,
+            "exact_route_sample": exact,
             "cpu_baseline": cpu,
             "cpu_baseline_reference_model": structured,
             "lib_build": build,

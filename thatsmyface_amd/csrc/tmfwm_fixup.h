@@ -97,74 +97,112 @@ TMF_DEVI void block_of(uint32_t id, uint32_t per_frame, int nbw, int64_t &fr, in
     bj = (int)(rem % (uint32_t)nbw);
 }
 
+// One listed block end to end on the dgesdd route, by G lanes (gl = this lane's index among
+// them) under lane policy Par: a group of a GroupPar wave, or a whole wave (WavePar, G = 64).
+template <int B, class Par, int G>
+TMF_DEVI void embed_fix_block(const EmbedArgs &a, uint32_t id, FixLds<B> &f, int gl)
+{
+    const uint32_t per_frame = (uint32_t)a.nbh * (uint32_t)a.nbw;
+    int64_t fr;
+    int bi, bj;
+    block_of(id, per_frame, a.nbw, fr, bi, bj);
+    const uint8_t *src = a.src + fr * a.frame_stride;
+    uint8_t *dst = a.dst + fr * a.frame_stride;
+    fix_load_dct<B, G>(src, a.W, bi, bj, f.D, gl);
+    const int info = lp::svd_f32_ws<true, Par>(f.D, runtime_n(B), nullptr, f.S, nullptr, f.ws);  // :195
+    if (info && gl == 0 && a.fb_bad) atomicAdd(a.fb_bad, 1u);
+    // :198 blend, :201 U @ (diag(S) @ Vt) as OpenBLAS sgemm's fma chain over k, on U and Vt
+    // rounded to f32 (numpy's astype) from the route's f64 U and VT
+    const double *U64 = f.ws + B * B, *VT64 = f.ws + 2 * B * B;
+    float *M = f.D;
+    const double w = (double)a.wm[(int64_t)bi * a.nbw + bj];
+    const float s0 = (float)((double)f.S[0] + a.alpha * (w / 255.0));
+    for (int e = gl; e < B * B; e += G) {
+        const int i = e / B, j = e % B;
+        float acc = 0.0f;
+#pragma unroll
+        for (int k = 0; k < B; ++k)
+            acc = __builtin_fmaf((float)U64[i + k * B], (k == 0 ? s0 : f.S[k]) * (float)VT64[k + j * B], acc);
+        M[e] = acc;
+    }
+    group_sync();
+    // :204 IDCT, axis 0 then axis 1
+    for (int c = gl; c < B; c += G) {
+        float col[B];
+#pragma unroll
+        for (int r = 0; r < B; ++r) col[r] = M[r * B + c];
+        dct::dct3<B>(col);
+#pragma unroll
+        for (int r = 0; r < B; ++r) M[r * B + c] = col[r];
+    }
+    group_sync();
+    for (int r = gl; r < B; r += G) {
+        float row[B];
+#pragma unroll
+        for (int c = 0; c < B; ++c) row[c] = M[r * B + c];
+        dct::dct3<B>(row);
+#pragma unroll
+        for (int c = 0; c < B; ++c) M[r * B + c] = row[c];
+    }
+    group_sync();
+    // :207-216 write back with the pixel's own chroma, inverse colour
+    for (int k = gl; k < B * B; k += G) {
+        const int64_t off = ((int64_t)(bi * B + k / B) * a.W + (int64_t)bj * B + k % B) * 3;
+        float cbs, crs;
+        chroma(src[off], src[off + 1], src[off + 2], cbs, crs);
+        uint32_t R8, G8, B8;
+        colour_inv(M[k], cbs, crs, R8, G8, B8);
+        dst[off] = (uint8_t)R8;
+        dst[off + 1] = (uint8_t)G8;
+        dst[off + 2] = (uint8_t)B8;
+    }
+    group_sync();  // the LDS slots are reused by the next listed block
+}
+
+template <int B, class Par, int G>
+TMF_DEVI void extract_fix_block(const ExtractArgs &a, uint32_t id, FixLds<B> &f, int gl)
+{
+    const uint32_t per_frame = (uint32_t)a.nbh * (uint32_t)a.nbw;
+    int64_t fr;
+    int bi, bj;
+    block_of(id, per_frame, a.nbw, fr, bi, bj);
+    float sig[2];
+    for (int img = 0; img < 2; ++img) {
+        fix_load_dct<B, G>((img == 0 ? a.wsrc : a.osrc) + fr * a.frame_stride, a.W, bi, bj, f.D, gl);
+        const int info = lp::svd_f32_ws<false, Par>(f.D, runtime_n(B), nullptr, f.S, nullptr, f.ws);  // :279-282
+        if (info && gl == 0 && a.fb_bad) atomicAdd(a.fb_bad, 1u);
+        sig[img] = f.S[0];
+        group_sync();
+    }
+    // :285-289 (numpy-2 NEP 50): f32 difference / f32(alpha); clip and *255 in f64; truncate
+    if (gl == 0) {
+        const float e = (sig[0] - sig[1]) / a.alpha32;
+        double d = (double)e;
+        d = d < 0.0 ? 0.0 : d;
+        d = d > 1.0 ? 1.0 : d;
+        a.out[fr * a.tile_stride + (int64_t)bi * a.nbw + bj] = (uint8_t)(uint32_t)(d * 255.0);
+    }
+}
+
+// A short list (the hybrid route's few flagged blocks: no more than the grid's workgroups) takes
+// a whole wave per block -- the lowest latency per block, and the pass is one block's latency;
+// a long one (the reference route: every block) takes 64 / G blocks per wave for throughput.
+// The choice is uniform over the grid (the device-side count against the grid size).
 template <int B>
 __global__ __launch_bounds__(64) void embed_fixup_kernel(EmbedArgs a, const uint32_t *__restrict__ list, const uint32_t *__restrict__ count)
 {
     constexpr int G = kFixLanes<B>, NG = 64 / G;
     static_assert(G >= B, "a group holds one element of dbdsqr's vectors per lane");
-    using Par = lp::GroupPar<G>;
     __shared__ FixLds<B> fl[NG];
-    const int gl = Par::lane(), grp = (int)(threadIdx.x / G);
-    FixLds<B> &f = fl[grp];
     const uint32_t n = *count;
-    const uint32_t per_frame = (uint32_t)a.nbh * (uint32_t)a.nbw;
+    if (n <= gridDim.x) {
+        if (blockIdx.x < n) embed_fix_block<B, lp::WavePar, 64>(a, list[blockIdx.x], fl[0], (int)threadIdx.x);
+        return;
+    }
+    const int gl = lp::GroupPar<G>::lane(), grp = (int)(threadIdx.x / G);
     for (uint32_t t0 = blockIdx.x * NG; t0 < n; t0 += gridDim.x * NG) {
         const uint32_t t = t0 + (uint32_t)grp;
-        if (t >= n) continue;  // this group has no block in this round
-        int64_t fr;
-        int bi, bj;
-        block_of(list[t], per_frame, a.nbw, fr, bi, bj);
-        const uint8_t *src = a.src + fr * a.frame_stride;
-        uint8_t *dst = a.dst + fr * a.frame_stride;
-        fix_load_dct<B, G>(src, a.W, bi, bj, f.D, gl);
-        const int info = lp::svd_f32_ws<true, Par>(f.D, runtime_n(B), nullptr, f.S, nullptr, f.ws);  // :195
-        if (info && gl == 0 && a.fb_bad) atomicAdd(a.fb_bad, 1u);
-        // :198 blend, :201 U @ (diag(S) @ Vt) as OpenBLAS sgemm's fma chain over k, on U and Vt
-        // rounded to f32 (numpy's astype) from the route's f64 U and VT
-        const double *U64 = f.ws + B * B, *VT64 = f.ws + 2 * B * B;
-        float *M = f.D;
-        const double w = (double)a.wm[(int64_t)bi * a.nbw + bj];
-        const float s0 = (float)((double)f.S[0] + a.alpha * (w / 255.0));
-        for (int e = gl; e < B * B; e += G) {
-            const int i = e / B, j = e % B;
-            float acc = 0.0f;
-#pragma unroll
-            for (int k = 0; k < B; ++k)
-                acc = __builtin_fmaf((float)U64[i + k * B], (k == 0 ? s0 : f.S[k]) * (float)VT64[k + j * B], acc);
-            M[e] = acc;
-        }
-        group_sync();
-        // :204 IDCT, axis 0 then axis 1
-        for (int c = gl; c < B; c += G) {
-            float col[B];
-#pragma unroll
-            for (int r = 0; r < B; ++r) col[r] = M[r * B + c];
-            dct::dct3<B>(col);
-#pragma unroll
-            for (int r = 0; r < B; ++r) M[r * B + c] = col[r];
-        }
-        group_sync();
-        for (int r = gl; r < B; r += G) {
-            float row[B];
-#pragma unroll
-            for (int c = 0; c < B; ++c) row[c] = M[r * B + c];
-            dct::dct3<B>(row);
-#pragma unroll
-            for (int c = 0; c < B; ++c) M[r * B + c] = row[c];
-        }
-        group_sync();
-        // :207-216 write back with the pixel's own chroma, inverse colour
-        for (int k = gl; k < B * B; k += G) {
-            const int64_t off = ((int64_t)(bi * B + k / B) * a.W + (int64_t)bj * B + k % B) * 3;
-            float cbs, crs;
-            chroma(src[off], src[off + 1], src[off + 2], cbs, crs);
-            uint32_t R8, G8, B8;
-            colour_inv(M[k], cbs, crs, R8, G8, B8);
-            dst[off] = (uint8_t)R8;
-            dst[off + 1] = (uint8_t)G8;
-            dst[off + 2] = (uint8_t)B8;
-        }
-        group_sync();  // the group's LDS slots are reused by its next listed block
+        if (t < n) embed_fix_block<B, lp::GroupPar<G>, G>(a, list[t], fl[grp], gl);  // else: no block this round
     }
 }
 
@@ -174,34 +212,16 @@ __global__ __launch_bounds__(64) void extract_fixup_kernel(ExtractArgs a, const 
 {
     constexpr int G = kFixLanes<B>, NG = 64 / G;
     static_assert(G >= B, "a group holds one element of dbdsqr's vectors per lane");
-    using Par = lp::GroupPar<G>;
     __shared__ FixLds<B> fl[NG];
-    const int gl = Par::lane(), grp = (int)(threadIdx.x / G);
-    FixLds<B> &f = fl[grp];
     const uint32_t n = *count;
-    const uint32_t per_frame = (uint32_t)a.nbh * (uint32_t)a.nbw;
+    if (n <= gridDim.x) {
+        if (blockIdx.x < n) extract_fix_block<B, lp::WavePar, 64>(a, list[blockIdx.x], fl[0], (int)threadIdx.x);
+        return;
+    }
+    const int gl = lp::GroupPar<G>::lane(), grp = (int)(threadIdx.x / G);
     for (uint32_t t0 = blockIdx.x * NG; t0 < n; t0 += gridDim.x * NG) {
         const uint32_t t = t0 + (uint32_t)grp;
-        if (t >= n) continue;
-        int64_t fr;
-        int bi, bj;
-        block_of(list[t], per_frame, a.nbw, fr, bi, bj);
-        float sig[2];
-        for (int img = 0; img < 2; ++img) {
-            fix_load_dct<B, G>((img == 0 ? a.wsrc : a.osrc) + fr * a.frame_stride, a.W, bi, bj, f.D, gl);
-            const int info = lp::svd_f32_ws<false, Par>(f.D, runtime_n(B), nullptr, f.S, nullptr, f.ws);  // :279-282
-            if (info && gl == 0 && a.fb_bad) atomicAdd(a.fb_bad, 1u);
-            sig[img] = f.S[0];
-            group_sync();
-        }
-        // :285-289 (numpy-2 NEP 50): f32 difference / f32(alpha); clip and *255 in f64; truncate
-        if (gl == 0) {
-            const float e = (sig[0] - sig[1]) / a.alpha32;
-            double d = (double)e;
-            d = d < 0.0 ? 0.0 : d;
-            d = d > 1.0 ? 1.0 : d;
-            a.out[fr * a.tile_stride + (int64_t)bi * a.nbw + bj] = (uint8_t)(uint32_t)(d * 255.0);
-        }
+        if (t < n) extract_fix_block<B, lp::GroupPar<G>, G>(a, list[t], fl[grp], gl);
     }
 }
 
