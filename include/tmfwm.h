@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define TMFWM_ABI_VERSION 7
+#define TMFWM_ABI_VERSION 8
 
 #define TMFWM_MEM_HOST 0
 #define TMFWM_MEM_DEVICE 1
@@ -140,6 +140,30 @@ int tmfwm_extract_ex(const uint8_t *wm_rgb, const uint8_t *orig_rgb, int64_t n_f
 int tmfwm_extract_route(const uint8_t *wm_rgb, const uint8_t *orig_rgb, int64_t n_frames, int32_t height, int32_t width,
                         int64_t frame_stride, int32_t block, double alpha, uint8_t *out_tiles, int32_t mem_kind,
                         void *hip_stream, int32_t route, int64_t *n_lapack_blocks);
+
+/* Pixel layouts of tmfwm_embed_px / tmfwm_extract_px (ABI 8) */
+#define TMFWM_PIX_RGB 3  /* 3 bytes per pixel, R G B (numpy / Image.tobytes order) */
+#define TMFWM_PIX_RGBX 4 /* 4 bytes per pixel, R G B pad: how PIL holds a mode-"RGB" image in memory
+                            (Image.__arrow_c_array__ / Image.fromarrow share it without a copy);
+                            the pad byte is ignored on input and written as 255 */
+
+/*
+ * tmfwm_embed_route with a pixel layout per side (ABI 8): the input frames have
+ * in_pixel_bytes per pixel (TMFWM_PIX_*) and in_frame_stride bytes between frames, the
+ * output out_pixel_bytes and out_frame_stride.  The bytes of every pixel's R, G, B are
+ * tmfwm_embed's.  4-byte frames are converted on the device, so the drop-in hands PIL's
+ * own image memory to the library and wraps the output as an image without a host-side
+ * pack or unpack.  3 -> 3 is tmfwm_embed_route (one frame stride for both).
+ */
+int tmfwm_embed_px(const uint8_t *rgb, int32_t in_pixel_bytes, int64_t in_frame_stride, int64_t n_frames, int32_t height,
+                   int32_t width, const uint8_t *wm_tile, int32_t block, double alpha, uint8_t *out, int32_t out_pixel_bytes,
+                   int64_t out_frame_stride, int32_t mem_kind, void *hip_stream, int32_t route, int64_t *n_lapack_blocks);
+
+/* tmfwm_extract_route with a pixel layout and frame stride per input image (ABI 8). */
+int tmfwm_extract_px(const uint8_t *wm_rgb, int32_t wm_pixel_bytes, int64_t wm_frame_stride, const uint8_t *orig_rgb,
+                     int32_t orig_pixel_bytes, int64_t orig_frame_stride, int64_t n_frames, int32_t height, int32_t width,
+                     int32_t block, double alpha, uint8_t *out_tiles, int32_t mem_kind, void *hip_stream, int32_t route,
+                     int64_t *n_lapack_blocks);
 
 /*
  * Multi-GPU embed / extract for callers without torch.distributed (one process drives

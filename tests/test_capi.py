@@ -38,7 +38,7 @@ def test_nm_exports_match_header():
 
 def test_abi_version_and_device_count():
     L = _lib.load()
-    assert L.tmfwm_abi_version() == _lib.ABI_VERSION == 7
+    assert L.tmfwm_abi_version() == _lib.ABI_VERSION == 8
     assert _lib.device_count() >= 0
 
 
@@ -64,6 +64,28 @@ def test_argument_validation_before_device():
         with pytest.raises(ValueError, match="route"):
             _lib.check(L.tmfwm_extract_route(p(a), p(a), 1, 16, 16, a.size, 8, 0.1, p(t), _lib.MEM_HOST, None, bad_route, None), "x")
     assert [L.tmfwm_embed_list_pass(k) for k in (4, 6, 8, 10, 12, 14, 16, 7, 18)] == [0, 0, 1, 0, 0, 0, 0, 0, 0]
+    # 4-byte pixel entry points (ABI 8): layouts and strides checked before any device work
+    a4 = np.zeros((16, 16, 4), np.uint8)
+    o4 = np.empty_like(a4)
+    for px in (2, 5):
+        with pytest.raises(ValueError, match="pixel bytes"):
+            _lib.check(L.tmfwm_embed_px(p(a4), px, a4.size, 1, 16, 16, p(t), 8, 0.1, p(o4), 4, o4.size, _lib.MEM_HOST, None, 0,
+                                        None), "embed_px")
+    with pytest.raises(ValueError, match="frame_stride"):  # a 4-byte frame needs H*W*4 bytes
+        _lib.check(L.tmfwm_embed_px(p(a4), 4, a.size, 1, 16, 16, p(t), 8, 0.1, p(o4), 4, o4.size, _lib.MEM_HOST, None, 0, None),
+                   "embed_px")
+    with pytest.raises(ValueError, match="one frame_stride"):  # 3 -> 3 is tmfwm_embed_route
+        _lib.check(L.tmfwm_embed_px(p(a), 3, a.size, 1, 16, 16, p(t), 8, 0.1, p(o), 3, a.size + 4, _lib.MEM_HOST, None, 0, None),
+                   "embed_px")
+    with pytest.raises(NotImplementedError):
+        _lib.check(L.tmfwm_embed_px(p(a4), 4, a4.size, 1, 16, 16, p(t), 7, 0.1, p(o4), 4, o4.size, _lib.MEM_HOST, None, 0, None),
+                   "embed_px")
+    with pytest.raises(ValueError, match="alpha"):
+        _lib.check(L.tmfwm_extract_px(p(a4), 4, a4.size, p(a), 3, a.size, 1, 16, 16, 8, 0.0, p(t), _lib.MEM_HOST, None, 0, None),
+                   "extract_px")
+    with pytest.raises(ValueError, match="original frame_stride"):
+        _lib.check(L.tmfwm_extract_px(p(a4), 4, a4.size, p(a), 4, a.size, 1, 16, 16, 8, 0.1, p(t), _lib.MEM_HOST, None, 0, None),
+                   "extract_px")
     with pytest.raises(ValueError):
         _lib.route_code("exact")
     assert (_lib.route_code("hybrid"), _lib.route_code("reference")) == (_lib.ROUTE_HYBRID, _lib.ROUTE_REFERENCE) == (0, 1)

@@ -844,3 +844,106 @@ def test_hybrid_vs_reference_route_4k(dev, b):
         assert nb == 0 and torch.equal(oh, orf)
     else:
         assert nb <= 4 and int((oh != orf).sum()) <= 4 * 3, nb
+
+
+@pytest.mark.parametrize("mem", ["host", "device"])
+def test_pixel_layouts_px_entry_points(dev, mem):
+    """tmfwm_embed_px / tmfwm_extract_px (ABI 8): 4-byte (PIL RGBX) and 3-byte frames in any
+    combination, padded frame strides, widths whose pixel count is not a multiple of 4 -- the
+    R, G, B bytes equal tmfwm_embed_route's, the pad byte is 255, extract equals tmfwm_extract_route."""
+    from thatsmyface_amd import _lib
+
+    L = _lib.load()
+    b, H, W, n = 8, 37, 61, 2  # 2257 pixels per frame: a partial quad at the end
+    rgb = _u8(910, (n, H, W, 3))
+    t = _u8(911, (H // b, W // b))
+    pad4, pad3 = 48, 20
+    f4, f3 = H * W * 4 + pad4, H * W * 3 + pad3
+    rgbx = np.full((n, f4), 77, np.uint8)
+    rgbx[:, : H * W * 4].reshape(n, H * W, 4)[..., :3] = rgb.reshape(n, H * W, 3)
+    rgb3 = np.zeros((n, f3), np.uint8)
+    rgb3[:, : H * W * 3] = rgb.reshape(n, -1)
+    ref = np.empty_like(rgb3)
+    _lib.check(L.tmfwm_embed_route(rgb3.ctypes.data, n, H, W, f3, t.ctypes.data, b, 0.1, ref.ctypes.data, _lib.MEM_HOST, None, 0,
+                                   None), "embed")
+    ref = ref[:, : H * W * 3].reshape(n, H * W, 3)
+    refx = np.empty((n, H // b, W // b), np.uint8)
+    ref3 = np.zeros((n, f3), np.uint8)
+    ref3[:, : H * W * 3] = ref.reshape(n, -1)
+    _lib.check(L.tmfwm_extract_route(ref3.ctypes.data, rgb3.ctypes.data, n, H, W, f3, b, 0.1, refx.ctypes.data, _lib.MEM_HOST, None,
+                                     0, None), "x")
+    srcs = {4: (rgbx, f4), 3: (rgb3, f3)}
+    for ipx in (3, 4):
+        for opx in (3, 4):
+            if ipx == opx == 3:
+                continue
+            src, sstride = srcs[ipx]
+            ostride = H * W * opx + 16
+            out = np.zeros((n, ostride), np.uint8)
+            if mem == "host":
+                _lib.check(L.tmfwm_embed_px(src.ctypes.data, ipx, sstride, n, H, W, t.ctypes.data, b, 0.1, out.ctypes.data, opx,
+                                            ostride, _lib.MEM_HOST, None, 0, None), "embed_px")
+            else:
+                ds, dt, do = (torch.from_numpy(x).to(dev) for x in (src, t, out))
+                _lib.check(L.tmfwm_embed_px(ds.data_ptr(), ipx, sstride, n, H, W, dt.data_ptr(), b, 0.1, do.data_ptr(), opx, ostride,
+                                            _lib.MEM_DEVICE, None, 0, None), "embed_px")
+                torch.cuda.synchronize()
+                out = do.cpu().numpy()
+            px = out[:, : H * W * opx].reshape(n, H * W, opx)
+            assert np.array_equal(px[..., :3], ref), (ipx, opx)
+            if opx == 4:
+                assert (px[..., 3] == 255).all()
+            assert (out[:, H * W * opx:] == 0).all()  # nothing written past a frame
+            # extract from the 4-/3-byte output against the cover in the other layout
+            x = np.empty((n, H // b, W // b), np.uint8)
+            osrc, ostr = srcs[3 if ipx == 4 else 4]
+            if mem == "host":
+                _lib.check(L.tmfwm_extract_px(out.ctypes.data, opx, ostride, osrc.ctypes.data, 3 if ipx == 4 else 4, ostr, n, H, W,
+                                              b, 0.1, x.ctypes.data, _lib.MEM_HOST, None, 0, None), "extract_px")
+            else:
+                dw, dor, dx = (torch.from_numpy(v).to(dev) for v in (out, osrc, x))
+                _lib.check(L.tmfwm_extract_px(dw.data_ptr(), opx, ostride, dor.data_ptr(), 3 if ipx == 4 else 4, ostr, n, H, W, b,
+                                              0.1, dx.data_ptr(), _lib.MEM_DEVICE, None, 0, None), "extract_px")
+                torch.cuda.synchronize()
+                x = dx.cpu().numpy()
+            assert np.array_equal(x, refx), (ipx, opx)
+
+
+def test_dropin_zero_copy_pil_path(dev, monkeypatch):
+    """The drop-in's zero-copy PIL path (RGBX in and out) returns the same images as
+    the copying path; an edited output image is read with its edits; pooled output buffers are
+    reused only once their image is gone; large (multi-block) covers fall back to np.asarray."""
+    import gc
+
+    from thatsmyface_amd import watermarking as W
+
+    cfg = {"block_size": 8, "alpha": 0.1}
+    wm = Image.fromarray(_u8(920, (40, 40)), "L")
+    for h, w in ((270, 484), (2160, 3840)):
+        cover = Image.fromarray(_u8(921, (h, w, 3)))
+        monkeypatch.setattr(W, "_zero_copy", True)
+        out = W.embed_watermark(cover, wm, False, cfg)
+        assert out.mode == "RGB" and out.size == cover.size
+        got = np.asarray(out)
+        ext = np.asarray(W.extract_watermark(out, cover, cfg))
+        monkeypatch.setattr(W, "_zero_copy", False)
+        assert np.array_equal(got, np.asarray(W.embed_watermark(cover, wm, False, cfg)))
+        assert np.array_equal(ext, np.asarray(W.extract_watermark(Image.fromarray(got), cover, cfg)))
+        monkeypatch.setattr(W, "_zero_copy", True)
+        # an in-place edit makes PIL copy the pixels first: extract must see the edit
+        out.paste((255, 0, 0), (0, 0, 64, 64))
+        edited = np.asarray(out)
+        monkeypatch.setattr(W, "_zero_copy", False)
+        want = np.asarray(W.extract_watermark(Image.fromarray(edited), cover, cfg))
+        monkeypatch.setattr(W, "_zero_copy", True)
+        assert np.array_equal(np.asarray(W.extract_watermark(out, cover, cfg)), want)
+    # pool: a live output keeps its buffer; a dropped one gives it back
+    cover = Image.fromarray(_u8(922, (64, 96, 3)))
+    a = W.embed_watermark(cover, wm, False, cfg)
+    b2 = W.embed_watermark(cover, wm, False, cfg)
+    assert a._tmfwm_rgbx is not b2._tmfwm_rgbx
+    buf = b2._tmfwm_rgbx.ctypes.data
+    del b2
+    gc.collect()
+    c = W.embed_watermark(cover, wm, False, cfg)
+    assert c._tmfwm_rgbx.ctypes.data == buf and np.array_equal(np.asarray(c), np.asarray(a))

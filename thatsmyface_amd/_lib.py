@@ -14,7 +14,7 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # TMFWM_LIB selects an alternative build (e.g. the phase-profile libtmfwm_stamps.so)
 LIB_PATH = os.environ.get("TMFWM_LIB") or os.path.join(_HERE, "libtmfwm.so")
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 MEM_HOST = 0
 MEM_DEVICE = 1
@@ -29,6 +29,10 @@ ERR_NODATA = -61
 ROUTE_HYBRID = 0  # TMFWM_ROUTE_*: the SVD route of embed / extract (include/tmfwm.h)
 ROUTE_REFERENCE = 1
 ROUTES = {"hybrid": ROUTE_HYBRID, "reference": ROUTE_REFERENCE}
+
+# pixel layouts of tmfwm_embed_px / tmfwm_extract_px (include/tmfwm.h, ABI 8)
+PIX_RGB = 3
+PIX_RGBX = 4  # PIL's in-memory mode "RGB" (R, G, B, pad)
 
 
 def route_code(route) -> int:
@@ -65,6 +69,8 @@ SIGNATURES = {
     "tmfwm_extract_ex": (ctypes.c_int, [_VP, _VP, _I64, _I32, _I32, _I64, _I32, _D, _VP, _I32, _VP, _VP]),
     "tmfwm_embed_route": (ctypes.c_int, [_VP, _I64, _I32, _I32, _I64, _VP, _I32, _D, _VP, _I32, _VP, _I32, _VP]),
     "tmfwm_extract_route": (ctypes.c_int, [_VP, _VP, _I64, _I32, _I32, _I64, _I32, _D, _VP, _I32, _VP, _I32, _VP]),
+    "tmfwm_embed_px": (ctypes.c_int, [_VP, _I32, _I64, _I64, _I32, _I32, _VP, _I32, _D, _VP, _I32, _I64, _I32, _VP, _I32, _VP]),
+    "tmfwm_extract_px": (ctypes.c_int, [_VP, _I32, _I64, _VP, _I32, _I64, _I64, _I32, _I32, _I32, _D, _VP, _I32, _VP, _I32, _VP]),
     "tmfwm_embed_multi": (ctypes.c_int, [_VP, _I64, _I32, _I32, _I64, _VP, _I32, _D, _VP, _VP, _I32, _VP]),
     "tmfwm_extract_multi": (ctypes.c_int, [_VP, _VP, _I64, _I32, _I32, _I64, _I32, _D, _VP, _VP, _I32, _VP]),
     "tmfwm_rgb_to_ycbcr": (ctypes.c_int, [_VP, _I64, _VP, _I32, _VP]),

@@ -575,6 +575,195 @@ int tmfwm_extract(const uint8_t *wm_rgb, const uint8_t *orig_rgb, int64_t n_fram
                             hip_stream, nullptr);
 }
 
+// ---- 4-byte pixels (ABI 8): the core runs on compact RGB device buffers; RGBX inputs are
+// packed and RGBX outputs unpacked on the device (tmfwm_pixels.hip)
+extern "C++" {
+namespace {
+int check_px(int32_t px, int64_t stride, int32_t H, int32_t W, const char *what)
+{
+    if (px != TMFWM_PIX_RGB && px != TMFWM_PIX_RGBX) return fail(TMFWM_ERR_INVALID, "%s pixel bytes %d (3 or 4)", what, px);
+    if (stride < (int64_t)H * W * px) return fail(TMFWM_ERR_INVALID, "%s frame_stride %lld < H*W*%d", what, (long long)stride, px);
+    return 0;
+}
+
+// frames (host or device, 3 or 4 bytes per pixel) -> device RGB with stride *s3; buf / tmp own
+// whatever had to be allocated
+int device_rgb(const uint8_t *src, int32_t px, int64_t stride, int64_t n, int32_t H, int32_t W, int32_t mem_kind,
+               hipStream_t st, const char *what, DevBuf &buf, DevBuf &tmp, const uint8_t **out, int64_t *s3)
+{
+    const int64_t f3 = (int64_t)H * W * 3;
+    const size_t span = span_bytes(n, stride, (int64_t)H * W * px);
+    const uint8_t *p = src;
+    if (mem_kind == TMFWM_MEM_DEVICE) {
+        if (int rc = check_device_ptr(src, what)) return rc;
+    } else {
+        if (!src) return fail(TMFWM_ERR_INVALID, "NULL host pointer (%s)", what);
+        if (int rc = (px == 3 ? buf : tmp).alloc(span, st, what)) return rc;
+        p = static_cast<const uint8_t *>((px == 3 ? buf : tmp).p);
+        TMF_HIP(hipMemcpyAsync(const_cast<uint8_t *>(p), src, span, hipMemcpyHostToDevice, st));
+    }
+    if (px == 3) {
+        *out = p;
+        *s3 = stride;
+        return 0;
+    }
+    if (int rc = buf.alloc((size_t)(n * f3), st, what)) return rc;
+    TMF_HIP(tmf::launch_pack_rgbx(p, stride, static_cast<uint8_t *>(buf.p), f3, n, H, W, st));
+    *out = static_cast<const uint8_t *>(buf.p);
+    *s3 = f3;
+    return 0;
+}
+}  // namespace
+}  // extern "C++"
+
+int tmfwm_embed_px(const uint8_t *rgb, int32_t in_pixel_bytes, int64_t in_frame_stride, int64_t n_frames, int32_t height,
+                   int32_t width, const uint8_t *wm_tile, int32_t block, double alpha, uint8_t *out, int32_t out_pixel_bytes,
+                   int64_t out_frame_stride, int32_t mem_kind, void *hip_stream, int32_t route, int64_t *n_lapack_blocks)
+{
+    t_err.clear();
+    if (in_pixel_bytes == TMFWM_PIX_RGB && out_pixel_bytes == TMFWM_PIX_RGB) {
+        if (in_frame_stride != out_frame_stride) return fail(TMFWM_ERR_INVALID, "3-byte input and output need one frame_stride");
+        return tmfwm_embed_route(rgb, n_frames, height, width, in_frame_stride, wm_tile, block, alpha, out, mem_kind, hip_stream,
+                                 route, n_lapack_blocks);
+    }
+    if (route != TMFWM_ROUTE_HYBRID && route != TMFWM_ROUTE_REFERENCE) return fail(TMFWM_ERR_INVALID, "route %d", route);
+    if (n_lapack_blocks) {
+        *n_lapack_blocks = 0;
+        t_list_pass = 0;
+    }
+    if (int rc = check_frames(n_frames, height, width, (int64_t)height * width * 3, block)) return rc;
+    if (int rc = check_px(in_pixel_bytes, in_frame_stride, height, width, "input")) return rc;
+    if (int rc = check_px(out_pixel_bytes, out_frame_stride, height, width, "output")) return rc;
+    if (!std::isfinite(alpha)) return fail(TMFWM_ERR_INVALID, "alpha is not finite");
+    if (mem_kind != TMFWM_MEM_HOST && mem_kind != TMFWM_MEM_DEVICE) return fail(TMFWM_ERR_INVALID, "mem_kind %d", mem_kind);
+    if (int rc = need_device()) return rc;
+    if (n_frames == 0 || height == 0 || width == 0) return 0;
+    const int nbh = height / block, nbw = width / block;
+    const size_t tbytes = (size_t)nbh * nbw;
+    const int64_t f3 = (int64_t)height * width * 3, fo = (int64_t)height * width * out_pixel_bytes;
+    const size_t ospan = span_bytes(n_frames, out_frame_stride, fo);
+    hipStream_t st = pick_stream(hip_stream);
+    if (mem_kind == TMFWM_MEM_DEVICE) {
+        if (int rc = check_device_ptr(out, "out")) return rc;
+        if (ranges_overlap(rgb, span_bytes(n_frames, in_frame_stride, (int64_t)height * width * in_pixel_bytes), out, ospan))
+            return fail(TMFWM_ERR_INVALID, "out overlaps rgb (in-place embed is not supported)");
+        if (tbytes) {
+            if (int rc = check_device_ptr(wm_tile, "wm_tile")) return rc;
+        }
+    } else if (!out || (tbytes && !wm_tile)) {
+        return fail(TMFWM_ERR_INVALID, "NULL host pointer");
+    }
+    DevBuf src3, tmp, dst3, dst4, dwm;
+    const uint8_t *s3p = nullptr;
+    int64_t s3 = 0;
+    if (int rc = device_rgb(rgb, in_pixel_bytes, in_frame_stride, n_frames, height, width, mem_kind, st, "input frames", src3, tmp,
+                            &s3p, &s3))
+        return rc;
+    const uint8_t *wm = wm_tile;
+    if (mem_kind == TMFWM_MEM_HOST && tbytes) {
+        if (int rc = dwm.alloc(tbytes, st, "watermark tile")) return rc;
+        TMF_HIP(hipMemcpyAsync(dwm.p, wm_tile, tbytes, hipMemcpyHostToDevice, st));
+        wm = static_cast<const uint8_t *>(dwm.p);
+    }
+    if (int rc = dst3.alloc(span_bytes(n_frames, s3, f3), st, "output frames")) return rc;
+    tmf::EmbedArgs a = tmf::embed_args(n_frames, height, width, s3, block, alpha);
+    a.src = s3p;
+    a.dst = static_cast<uint8_t *>(dst3.p);
+    a.wm = wm;
+    a.aligned = tmf::dev_aligned(a.src, a.dst, s3, width);
+    if (int rc = tmf::run_embed(a, st, n_lapack_blocks, mem_kind == TMFWM_MEM_HOST, nullptr, route)) return rc;
+    uint8_t *o = out;  // device destination of the output's final layout
+    if (mem_kind == TMFWM_MEM_HOST) {
+        if (int rc = dst4.alloc(ospan, st, "output staging")) return rc;
+        o = static_cast<uint8_t *>(dst4.p);
+    }
+    if (out_pixel_bytes == TMFWM_PIX_RGBX)
+        TMF_HIP(tmf::launch_unpack_rgbx(a.dst, s3, o, out_frame_stride, n_frames, height, width, st));
+    else
+        TMF_HIP(hipMemcpy2DAsync(o, (size_t)out_frame_stride, a.dst, (size_t)s3, (size_t)f3, (size_t)n_frames,
+                                 hipMemcpyDeviceToDevice, st));
+    if (mem_kind == TMFWM_MEM_HOST) {  // the caller's bytes between frames stay as they are
+        if (n_frames == 1 || out_frame_stride == fo)
+            TMF_HIP(hipMemcpyAsync(out, o, ospan, hipMemcpyDeviceToHost, st));
+        else
+            TMF_HIP(hipMemcpy2DAsync(out, (size_t)out_frame_stride, o, (size_t)out_frame_stride, (size_t)fo, (size_t)n_frames,
+                                     hipMemcpyDeviceToHost, st));
+        TMF_HIP(hipStreamSynchronize(st));
+    }
+    return 0;
+}
+
+int tmfwm_extract_px(const uint8_t *wm_rgb, int32_t wm_pixel_bytes, int64_t wm_frame_stride, const uint8_t *orig_rgb,
+                     int32_t orig_pixel_bytes, int64_t orig_frame_stride, int64_t n_frames, int32_t height, int32_t width,
+                     int32_t block, double alpha, uint8_t *out_tiles, int32_t mem_kind, void *hip_stream, int32_t route,
+                     int64_t *n_lapack_blocks)
+{
+    t_err.clear();
+    if (wm_pixel_bytes == TMFWM_PIX_RGB && orig_pixel_bytes == TMFWM_PIX_RGB && wm_frame_stride == orig_frame_stride)
+        return tmfwm_extract_route(wm_rgb, orig_rgb, n_frames, height, width, wm_frame_stride, block, alpha, out_tiles, mem_kind,
+                                   hip_stream, route, n_lapack_blocks);
+    if (route != TMFWM_ROUTE_HYBRID && route != TMFWM_ROUTE_REFERENCE) return fail(TMFWM_ERR_INVALID, "route %d", route);
+    if (n_lapack_blocks) {
+        *n_lapack_blocks = 0;
+        t_list_pass = 0;
+    }
+    if (int rc = check_frames(n_frames, height, width, (int64_t)height * width * 3, block)) return rc;
+    if (int rc = check_px(wm_pixel_bytes, wm_frame_stride, height, width, "watermarked")) return rc;
+    if (int rc = check_px(orig_pixel_bytes, orig_frame_stride, height, width, "original")) return rc;
+    if (!std::isfinite(alpha) || alpha == 0.0) return fail(TMFWM_ERR_INVALID, "alpha must be finite and non-zero");
+    if (mem_kind != TMFWM_MEM_HOST && mem_kind != TMFWM_MEM_DEVICE) return fail(TMFWM_ERR_INVALID, "mem_kind %d", mem_kind);
+    if (int rc = need_device()) return rc;
+    const int nbh = height / block, nbw = width / block;
+    const int64_t tbytes = (int64_t)nbh * nbw, f3 = (int64_t)height * width * 3;
+    if (n_frames == 0 || tbytes == 0) return 0;
+    const size_t obytes = (size_t)(tbytes * n_frames);
+    hipStream_t st = pick_stream(hip_stream);
+    if (mem_kind == TMFWM_MEM_DEVICE) {
+        if (int rc = check_device_ptr(out_tiles, "out_tiles")) return rc;
+        if (ranges_overlap(out_tiles, obytes, wm_rgb, span_bytes(n_frames, wm_frame_stride, (int64_t)height * width * wm_pixel_bytes)) ||
+            ranges_overlap(out_tiles, obytes, orig_rgb, span_bytes(n_frames, orig_frame_stride, (int64_t)height * width * orig_pixel_bytes)))
+            return fail(TMFWM_ERR_INVALID, "out_tiles overlaps an input batch");
+    } else if (!out_tiles) {
+        return fail(TMFWM_ERR_INVALID, "NULL host pointer");
+    }
+    // both images as compact RGB (one frame stride for the kernels)
+    DevBuf w3, wtmp, o3, otmp, wc, oc, dout;
+    const uint8_t *wp = nullptr, *op = nullptr;
+    int64_t ws = 0, os = 0;
+    if (int rc = device_rgb(wm_rgb, wm_pixel_bytes, wm_frame_stride, n_frames, height, width, mem_kind, st, "watermarked frames", w3,
+                            wtmp, &wp, &ws))
+        return rc;
+    if (int rc = device_rgb(orig_rgb, orig_pixel_bytes, orig_frame_stride, n_frames, height, width, mem_kind, st, "original frames",
+                            o3, otmp, &op, &os))
+        return rc;
+    if (ws != f3) {
+        if (int rc = wc.alloc((size_t)(n_frames * f3), st, "watermarked frames")) return rc;
+        TMF_HIP(hipMemcpy2DAsync(wc.p, (size_t)f3, wp, (size_t)ws, (size_t)f3, (size_t)n_frames, hipMemcpyDeviceToDevice, st));
+        wp = static_cast<const uint8_t *>(wc.p);
+    }
+    if (os != f3) {
+        if (int rc = oc.alloc((size_t)(n_frames * f3), st, "original frames")) return rc;
+        TMF_HIP(hipMemcpy2DAsync(oc.p, (size_t)f3, op, (size_t)os, (size_t)f3, (size_t)n_frames, hipMemcpyDeviceToDevice, st));
+        op = static_cast<const uint8_t *>(oc.p);
+    }
+    tmf::ExtractArgs a = tmf::extract_args(n_frames, height, width, f3, block, alpha);
+    a.wsrc = wp;
+    a.osrc = op;
+    if (mem_kind == TMFWM_MEM_HOST) {
+        if (int rc = dout.alloc(obytes, st, "extracted tiles")) return rc;
+        a.out = static_cast<uint8_t *>(dout.p);
+    } else {
+        a.out = out_tiles;
+    }
+    a.aligned = tmf::dev_aligned(wp, op, f3, width);
+    if (int rc = tmf::run_extract(a, st, n_lapack_blocks, mem_kind == TMFWM_MEM_HOST, nullptr, route)) return rc;
+    if (mem_kind == TMFWM_MEM_HOST) {
+        TMF_HIP(hipMemcpyAsync(out_tiles, dout.p, obytes, hipMemcpyDeviceToHost, st));
+        TMF_HIP(hipStreamSynchronize(st));
+    }
+    return 0;
+}
+
 extern "C++" {
 namespace {
 

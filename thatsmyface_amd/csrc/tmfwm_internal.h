@@ -86,6 +86,12 @@ hipError_t launch_embed_fixup(const EmbedArgs &a, const uint32_t *list, const ui
 hipError_t launch_extract_fixup(const ExtractArgs &a, const uint32_t *list, const uint32_t *count, int64_t max_entries, hipStream_t st);
 // the reference route: list = 0 .. n-1, *count = n (every block of a launch on the dgesdd route)
 hipError_t launch_list_all(uint32_t *list, uint32_t *count, int64_t n, hipStream_t st);
+// RGBX (4 bytes per pixel, PIL's in-memory "RGB") <-> RGB (3 bytes) per frame (tmfwm_pixels.hip);
+// strides in bytes between frames; unpack writes 255 into the pad byte
+hipError_t launch_pack_rgbx(const uint8_t *src4, int64_t sstride, uint8_t *dst3, int64_t dstride, int64_t n, int H, int W,
+                            hipStream_t st);
+hipError_t launch_unpack_rgbx(const uint8_t *src3, int64_t sstride, uint8_t *dst4, int64_t dstride, int64_t n, int H, int W,
+                              hipStream_t st);
 hipError_t launch_lapack_svd_blocks(const float *D, int64_t nb, int block, float *U, float *S, float *Vt, int want_v, int32_t *info,
                                     hipStream_t st);
 hipError_t launch_lapack_nrm2(const double *x, int64_t nvec, int n, int inc, double *out, hipStream_t st);

@@ -22,6 +22,7 @@ import ctypes
 import hashlib
 import io
 import os
+import sys
 import threading
 
 import numpy as np
@@ -184,9 +185,73 @@ def _rgb_image(img):
 _TILE_CACHE_MAX = 16
 _tile_cache: "dict[tuple, np.ndarray]" = {}
 _tile_lock = threading.Lock()
-# Per-thread output staging of embed_watermark: Image.fromarray copies an RGB array into PIL's
-# own storage, so the array is reused by the thread's next call (no fresh pages to fault in).
+# Per-thread output staging of embed_watermark's copying path: Image.fromarray copies an RGB
+# array into PIL's own storage, so the array is reused by the thread's next call.
 _tls = threading.local()
+
+# Zero-copy PIL path: PIL holds a mode-"RGB" image as 4 bytes per pixel; pyarrow
+# hands that memory over (Image.__arrow_c_array__) and Image.fromarrow wraps 4-byte output
+# memory as an RGB image, so tmfwm_embed_px / tmfwm_extract_px read and write PIL's own layout
+# and the host never packs or unpacks pixels.  Inputs Pillow stores in several blocks (large
+# images) and read-only (mapped / arrow-backed) images -- Pillow 12.2's __arrow_c_array__
+# crashes on those -- take np.asarray instead.  TMFWM_PIL_ZERO_COPY=0 turns the path off.
+_zero_copy = os.environ.get("TMFWM_PIL_ZERO_COPY", "1") != "0"
+_pa = None
+_POOL_KEEP = 4  # free RGBX output buffers kept per size
+_out_pool: "dict[int, list[np.ndarray]]" = {}
+_pool_lock = threading.Lock()
+
+
+def _arrow():
+    global _pa, _zero_copy
+    if _pa is None and _zero_copy:
+        try:
+            import pyarrow  # noqa: PLC0415
+
+            _pa = pyarrow
+        except ImportError:
+            _zero_copy = False
+    return _pa if _zero_copy else None
+
+
+def _rgbx_view(image):
+    """(address, keepalive) of PIL's own 4-byte pixels of an RGB image, or None."""
+    own = getattr(image, "_tmfwm_rgbx", None)  # an embed_watermark output: its buffer as it is,
+    if own is not None and image.readonly:  # unless PIL copied it (every in-place edit does first)
+        return _ptr(own), own
+    pa = _arrow()
+    if pa is None or image.readonly or not hasattr(image, "__arrow_c_array__"):
+        return None
+    try:
+        arr = pa.array(image)
+    except (ValueError, TypeError, NotImplementedError):  # several memory blocks
+        return None
+    vals = arr.values
+    if len(vals) != image.width * image.height * 4:
+        return None
+    return vals.buffers()[1].address + vals.offset, arr
+
+
+def _take_out(nbytes: int) -> np.ndarray:
+    """An RGBX output buffer: a pooled one nothing else references (its image is gone), else new."""
+    with _pool_lock:
+        lst = _out_pool.setdefault(nbytes, [])
+        for b in lst:
+            if sys.getrefcount(b) == 3:  # the list, this loop's name and the call's argument
+                return b
+        b = np.empty(nbytes, np.uint8)
+        if len(lst) < _POOL_KEEP:
+            lst.append(b)
+        return b
+
+
+def _rgb_from_rgbx(buf: np.ndarray, width: int, height: int):
+    """Image.fromarrow over the RGBX buffer: a mode-"RGB" image sharing its memory."""
+    pa = _pa
+    vals = pa.Array.from_buffers(pa.uint8(), width * height * 4, [None, pa.py_buffer(buf)])
+    img = Image.fromarrow(pa.FixedSizeListArray.from_arrays(vals, 4), "RGB", (width, height))
+    img._tmfwm_rgbx = buf  # extract_watermark reads it back without an export
+    return img
 
 
 def _tile_for(watermark_data, nbh, nbw, preserve_ratio) -> np.ndarray:
@@ -210,13 +275,30 @@ def embed_watermark(image, watermark_data, preserve_ratio=False, custom_settings
     """watermarking.py:135-221: returns a new RGB PIL image of the same size."""
     block_size, alpha = _settings(custom_settings)
     image = _rgb_image(image)
-    rgb = np.ascontiguousarray(np.asarray(image, dtype=np.uint8))
-    height, width = rgb.shape[:2]
     block_size = int(block_size)
     if block_size <= 0:
         raise ValueError(f"block_size must be positive, got {block_size}")
+    width, height = image.size
     nbh, nbw = height // block_size, width // block_size
     tile = _tile_for(watermark_data, nbh, nbw, preserve_ratio)
+    route = _route(custom_settings)
+    if _arrow() is not None and height > 0 and width > 0:
+        view = _rgbx_view(image)
+        if view is not None:
+            src, src_px, keep = view[0], _lib.PIX_RGBX, view[1]
+        else:
+            keep = np.ascontiguousarray(np.asarray(image, dtype=np.uint8))
+            src, src_px = _ptr(keep), _lib.PIX_RGB
+        out = _take_out(height * width * 4)
+        L = _lib.load()
+        _lib.check(
+            L.tmfwm_embed_px(src, src_px, height * width * src_px, 1, height, width, _ptr(tile), block_size, float(alpha),
+                             _ptr(out), _lib.PIX_RGBX, height * width * 4, _lib.MEM_HOST, None, route, None),
+            "embed_watermark",
+        )
+        del keep
+        return _rgb_from_rgbx(out, width, height)
+    rgb = np.ascontiguousarray(np.asarray(image, dtype=np.uint8))
     out = getattr(_tls, "out", None)
     if out is None or out.shape != rgb.shape:
         out = np.empty_like(rgb)
@@ -224,7 +306,7 @@ def embed_watermark(image, watermark_data, preserve_ratio=False, custom_settings
     L = _lib.load()
     _lib.check(
         L.tmfwm_embed_route(_ptr(rgb), 1, height, width, rgb.size, _ptr(tile), block_size, float(alpha), _ptr(out), _lib.MEM_HOST,
-                            None, _route(custom_settings), None),
+                            None, route, None),
         "embed_watermark",
     )
     img = Image.fromarray(out)
@@ -239,10 +321,33 @@ def extract_watermark(watermarked_image, original_image, custom_settings=None):
     block_size = int(block_size)
     if block_size <= 0:
         raise ValueError(f"block_size must be positive, got {block_size}")
-    w = np.asarray(_rgb_image(watermarked_image), dtype=np.uint8)
-    o = np.asarray(_rgb_image(original_image), dtype=np.uint8)
-    height, width = w.shape[:2]
+    wimg, oimg = _rgb_image(watermarked_image), _rgb_image(original_image)
+    width, height = wimg.size
     nbh, nbw = height // block_size, width // block_size
+    route = _route(custom_settings)
+    if _arrow() is not None and nbh > 0 and nbw > 0 and oimg.size == wimg.size:
+        ins = []
+        for img in (wimg, oimg):
+            view = _rgbx_view(img)
+            if view is None:
+                arr = np.ascontiguousarray(np.asarray(img, dtype=np.uint8))
+                view = (_ptr(arr), arr)
+                px = _lib.PIX_RGB
+            else:
+                px = _lib.PIX_RGBX
+            ins.append((view[0], px, view[1]))
+        out = np.empty((nbh, nbw), np.uint8)
+        L = _lib.load()
+        (wp, wpx, _), (op, opx, _) = ins
+        _lib.check(
+            L.tmfwm_extract_px(wp, wpx, height * width * wpx, op, opx, height * width * opx, 1, height, width, block_size,
+                               float(alpha), _ptr(out), _lib.MEM_HOST, None, route, None),
+            "extract_watermark",
+        )
+        del ins
+        return Image.fromarray(out)
+    w = np.asarray(wimg, dtype=np.uint8)
+    o = np.asarray(oimg, dtype=np.uint8)
     if nbh == 0 or nbw == 0:
         return Image.fromarray(np.zeros((nbh, nbw), np.uint8))
     if o.shape[0] < height or o.shape[1] < width:
@@ -255,7 +360,7 @@ def extract_watermark(watermarked_image, original_image, custom_settings=None):
     L = _lib.load()
     _lib.check(
         L.tmfwm_extract_route(_ptr(w), _ptr(o), 1, height, width, w.size, block_size, float(alpha), _ptr(out), _lib.MEM_HOST,
-                              None, _route(custom_settings), None),
+                              None, route, None),
         "extract_watermark",
     )
     return Image.fromarray(out)

@@ -58,6 +58,17 @@ def main():
     rs = dict(cs, svd_route="reference")
     out["embed_watermark_reference_route_ms"] = timed(lambda: W.embed_watermark(cover, png, True, rs))
     out["extract_watermark_reference_route_ms"] = timed(lambda: W.extract_watermark(wm_img, cover, rs))
+    # the extract page's inputs are decoded uploads, not embed_watermark's own output image
+    b2 = io.BytesIO()
+    wm_img.save(b2, format="PNG")
+    wm_dec = Image.open(io.BytesIO(b2.getvalue()))
+    wm_dec.load()
+    out["extract_watermark_decoded_ms"] = timed(lambda: W.extract_watermark(wm_dec, cover, cs))
+    # the copying path (np.asarray in, Image.fromarray out), for comparison
+    W._zero_copy = False
+    out["embed_watermark_copying_path_ms"] = timed(lambda: W.embed_watermark(cover, png, True, cs))
+    out["extract_watermark_copying_path_ms"] = timed(lambda: W.extract_watermark(wm_dec, cover, cs))
+    W._zero_copy = True
     # where embed_watermark's time goes (its stages, each timed alone)
     from thatsmyface_amd import _lib
     rgb = np.ascontiguousarray(np.asarray(cover.convert("RGB"), dtype=np.uint8))
@@ -65,6 +76,8 @@ def main():
     nbh, nbw = a.height // a.block, a.width // a.block
     tile = np.ascontiguousarray(np.asarray(W.resize_watermark(wimg, nbh, nbw, True), dtype=np.uint8))
     host_out = np.empty_like(rgb)
+    view = W._rgbx_view(cover)
+    out4 = np.empty(a.height * a.width * 4, np.uint8)
     L = _lib.load()
     stages = {
         "convert_rgb": lambda: cover.convert("RGB"),
@@ -74,7 +87,13 @@ def main():
         "tmfwm_embed_host": lambda: _lib.check(L.tmfwm_embed(rgb.ctypes.data, 1, a.height, a.width, rgb.size, tile.ctypes.data,
                                                              a.block, 0.1, host_out.ctypes.data, _lib.MEM_HOST, None), "embed"),
         "fromarray": lambda: Image.fromarray(host_out),
+        "rgbx_view": lambda: W._rgbx_view(cover),
+        "fromarrow": lambda: W._rgb_from_rgbx(out4, a.width, a.height),
     }
+    if view is not None:  # PIL holds the cover in one block (images up to ~16 MB)
+        stages["tmfwm_embed_px_host"] = lambda: _lib.check(
+            L.tmfwm_embed_px(view[0], 4, a.height * a.width * 4, 1, a.height, a.width, tile.ctypes.data, a.block, 0.1,
+                             out4.ctypes.data, 4, a.height * a.width * 4, _lib.MEM_HOST, None, 0, None), "px")
     out["embed_stages_ms"] = {k: timed(f) for k, f in stages.items()}
     dev = torch.device("cuda", 0)
     fr = torch.from_numpy(np.asarray(cover)[None].copy()).to(dev)

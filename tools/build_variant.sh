@@ -48,6 +48,6 @@ fi
 wait
 mkdir -p "$ROOT/variants"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$ROOT/variants/libtmfwm_$NAME.so" "$T/k.o" "$T/e8.o" \
-    "$C/tmfwm_capi.o" "$C/tmfwm_multi.o" "$C/tmfwm_qr.o" "$C/tmfwm_tile.o" $FB -fopenmp -ldl -lpthread
+    "$C/tmfwm_capi.o" "$C/tmfwm_multi.o" "$C/tmfwm_qr.o" "$C/tmfwm_tile.o" "$C/tmfwm_pixels.o" $FB -fopenmp -ldl -lpthread
 rm -rf "$T"
 echo "variants/libtmfwm_$NAME.so"
