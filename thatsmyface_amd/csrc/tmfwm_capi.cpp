@@ -225,6 +225,44 @@ int sum_counts(const uint32_t *dcounts, int64_t nchunks, hipStream_t st, int64_t
     return sum_host_counts(h.data(), nchunks, out);
 }
 
+// Pinned landing zones for the per-chunk counts of host-memory calls: the counts travel with the
+// call's last copy and are read after its one synchronisation (no extra round trip between the
+// kernels and the copy back).  A small process-wide free list, so no thread keeps pinned memory.
+constexpr int64_t kSinkChunks = 16;
+std::mutex g_sink_mu;
+std::vector<uint32_t *> g_sinks;
+
+struct HostSink {
+    uint32_t *p = nullptr;
+    hipStream_t st = nullptr;
+    HostSink(int64_t nchunks, hipStream_t s) : st(s)
+    {
+        if (nchunks > kSinkChunks) return;  // the synchronous read-back instead
+        {
+            std::lock_guard<std::mutex> g(g_sink_mu);
+            if (!g_sinks.empty()) {
+                p = g_sinks.back();
+                g_sinks.pop_back();
+                return;
+            }
+        }
+        if (hipHostMalloc(reinterpret_cast<void **>(&p), kSinkChunks * 12, hipHostMallocDefault) != hipSuccess) {
+            (void)hipGetLastError();
+            p = nullptr;
+        }
+    }
+    ~HostSink()
+    {
+        if (!p) return;
+        (void)hipStreamSynchronize(st);  // an error return may leave the copy into it in flight
+        (void)hipGetLastError();
+        std::lock_guard<std::mutex> g(g_sink_mu);
+        g_sinks.push_back(p);
+    }
+    HostSink(const HostSink &) = delete;
+    HostSink &operator=(const HostSink &) = delete;
+};
+
 }  // namespace
 
 namespace tmf {
@@ -483,7 +521,9 @@ int tmfwm_embed_route(const uint8_t *rgb, int64_t n_frames, int32_t height, int3
     a.dst = static_cast<uint8_t *>(dout.p);
     a.wm = static_cast<const uint8_t *>(dwm.p);
     a.aligned = frame_stride % 4 == 0 && width % 4 == 0;
-    if (int rc = tmf::run_embed(a, st, n_lapack_blocks, true, nullptr, route)) return rc;
+    const int64_t nch = tmf::count_chunks(n_frames, height, width, block);
+    HostSink sink(nch, st);
+    if (int rc = tmf::run_embed(a, st, n_lapack_blocks, true, sink.p, route)) return rc;
     if (frame_stride == fbytes) {
         TMF_HIP(hipMemcpyAsync(out, dout.p, span, hipMemcpyDeviceToHost, st));
     } else {
@@ -492,7 +532,7 @@ int tmfwm_embed_route(const uint8_t *rgb, int64_t n_frames, int32_t height, int3
                                    hipMemcpyDeviceToHost, st));
     }
     TMF_HIP(hipStreamSynchronize(st));
-    return 0;
+    return sink.p ? tmf::sum_sink(sink.p, nch, n_lapack_blocks) : 0;
 }
 
 int tmfwm_embed_ex(const uint8_t *rgb, int64_t n_frames, int32_t height, int32_t width, int64_t frame_stride,
@@ -554,10 +594,12 @@ int tmfwm_extract_route(const uint8_t *wm_rgb, const uint8_t *orig_rgb, int64_t 
     a.osrc = static_cast<const uint8_t *>(dor.p);
     a.out = static_cast<uint8_t *>(dout.p);
     a.aligned = frame_stride % 4 == 0 && width % 4 == 0;
-    if (int rc = tmf::run_extract(a, st, n_lapack_blocks, true, nullptr, route)) return rc;
+    const int64_t nch = tmf::count_chunks(n_frames, height, width, block);
+    HostSink sink(nch, st);
+    if (int rc = tmf::run_extract(a, st, n_lapack_blocks, true, sink.p, route)) return rc;
     TMF_HIP(hipMemcpyAsync(out_tiles, dout.p, (size_t)(tbytes * n_frames), hipMemcpyDeviceToHost, st));
     TMF_HIP(hipStreamSynchronize(st));
-    return 0;
+    return sink.p ? tmf::sum_sink(sink.p, nch, n_lapack_blocks) : 0;
 }
 
 int tmfwm_extract_ex(const uint8_t *wm_rgb, const uint8_t *orig_rgb, int64_t n_frames, int32_t height, int32_t width,
@@ -671,7 +713,9 @@ int tmfwm_embed_px(const uint8_t *rgb, int32_t in_pixel_bytes, int64_t in_frame_
     a.dst = static_cast<uint8_t *>(dst3.p);
     a.wm = wm;
     a.aligned = tmf::dev_aligned(a.src, a.dst, s3, width);
-    if (int rc = tmf::run_embed(a, st, n_lapack_blocks, mem_kind == TMFWM_MEM_HOST, nullptr, route)) return rc;
+    const int64_t nch = tmf::count_chunks(n_frames, height, width, block);
+    HostSink sink(mem_kind == TMFWM_MEM_HOST ? nch : kSinkChunks + 1, st);
+    if (int rc = tmf::run_embed(a, st, n_lapack_blocks, mem_kind == TMFWM_MEM_HOST, sink.p, route)) return rc;
     uint8_t *o = out;  // device destination of the output's final layout
     if (mem_kind == TMFWM_MEM_HOST) {
         if (int rc = dst4.alloc(ospan, st, "output staging")) return rc;
@@ -689,6 +733,7 @@ int tmfwm_embed_px(const uint8_t *rgb, int32_t in_pixel_bytes, int64_t in_frame_
             TMF_HIP(hipMemcpy2DAsync(out, (size_t)out_frame_stride, o, (size_t)out_frame_stride, (size_t)fo, (size_t)n_frames,
                                      hipMemcpyDeviceToHost, st));
         TMF_HIP(hipStreamSynchronize(st));
+        if (sink.p) return tmf::sum_sink(sink.p, nch, n_lapack_blocks);
     }
     return 0;
 }
@@ -756,10 +801,13 @@ int tmfwm_extract_px(const uint8_t *wm_rgb, int32_t wm_pixel_bytes, int64_t wm_f
         a.out = out_tiles;
     }
     a.aligned = tmf::dev_aligned(wp, op, f3, width);
-    if (int rc = tmf::run_extract(a, st, n_lapack_blocks, mem_kind == TMFWM_MEM_HOST, nullptr, route)) return rc;
+    const int64_t nch = tmf::count_chunks(n_frames, height, width, block);
+    HostSink sink(mem_kind == TMFWM_MEM_HOST ? nch : kSinkChunks + 1, st);
+    if (int rc = tmf::run_extract(a, st, n_lapack_blocks, mem_kind == TMFWM_MEM_HOST, sink.p, route)) return rc;
     if (mem_kind == TMFWM_MEM_HOST) {
         TMF_HIP(hipMemcpyAsync(out_tiles, dout.p, obytes, hipMemcpyDeviceToHost, st));
         TMF_HIP(hipStreamSynchronize(st));
+        if (sink.p) return tmf::sum_sink(sink.p, nch, n_lapack_blocks);
     }
     return 0;
 }

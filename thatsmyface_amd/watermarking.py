@@ -197,7 +197,7 @@ _tls = threading.local()
 # crashes on those -- take np.asarray instead.  TMFWM_PIL_ZERO_COPY=0 turns the path off.
 _zero_copy = os.environ.get("TMFWM_PIL_ZERO_COPY", "1") != "0"
 _pa = None
-_POOL_KEEP = 4  # free RGBX output buffers kept per size
+_POOL_KEEP = 4  # output buffers kept per size
 _out_pool: "dict[int, list[np.ndarray]]" = {}
 _pool_lock = threading.Lock()
 
@@ -233,7 +233,8 @@ def _rgbx_view(image):
 
 
 def _take_out(nbytes: int) -> np.ndarray:
-    """An RGBX output buffer: a pooled one nothing else references (its image is gone), else new."""
+    """An RGBX output buffer: a pooled one nothing else references (its image is gone), else new
+    (its pages are then faulted in once; page-locked buffers measured no faster, r04k)."""
     with _pool_lock:
         lst = _out_pool.setdefault(nbytes, [])
         for b in lst:
