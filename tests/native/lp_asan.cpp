@@ -1,6 +1,6 @@
 // TEST-ONLY: bounds check of the dgesdd route's workspace indexing (thatsmyface_amd/csrc/
 // tmfwm_lapack.h) under AddressSanitizer on the host.  Every array -- D, U, S, Vt and the
-// workspace of exactly ws_doubles(n) doubles, the size the fixup kernels give it in LDS --
+// workspace of exactly ws_doubles_for<want_v>(n) doubles, the size the fixup kernels give it in LDS --
 // is its own heap allocation of exactly its size, so any read or write past an end aborts.
 // Built and run by tests/test_lapack_device_code.py::test_workspace_bounds_asan; never shipped.
 #include "../../thatsmyface_amd/csrc/tmfwm_lapack.h"
@@ -46,7 +46,7 @@ static int run(int n, int kind, bool want_v)
     fill(D, n, kind);
     float *U = want_v ? new float[n * n] : nullptr, *Vt = want_v ? new float[n * n] : nullptr;
     float *S = new float[n];
-    double *ws = new double[ws_doubles(n)];
+    double *ws = new double[want_v ? ws_doubles_for<true>(n) : ws_doubles_for<false>(n)];  // as the fixup kernels size it
     const int info = want_v ? svd_f32_ws<true, P>(D, n, U, S, Vt, ws) : svd_f32_ws<false, P>(D, n, nullptr, S, nullptr, ws);
     delete[] ws;
     delete[] S;

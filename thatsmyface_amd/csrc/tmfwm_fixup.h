@@ -80,14 +80,19 @@ TMF_DEVI void fix_load_dct(const uint8_t *frame, int W, int bi, int bj, float *t
     group_sync();
 }
 
-// one group's LDS: the route's workspace (its U and VT, f64 column-major at ws + B^2 and
-// ws + 2 B^2, are read in place by the reconstruction), the DCT block D -- dead once the route
-// has copied it, so the reconstruction M reuses it -- and S
-template <int B>
-struct FixLds {
-    double ws[lp::ws_doubles(B)];
+// one group's LDS: the route's workspace (embed: its U and VT, f64 column-major at ws + B^2 and
+// ws + 2 B^2, are read in place by the reconstruction; extract: S only, no U and VT -- 1.4 KB
+// instead of 2.4 KB per b = 8 group, so LDS no longer caps the extract pass at 2 waves / SIMD),
+// the DCT block D -- dead once the route has copied it, so the reconstruction M reuses it -- and S
+template <int B, bool WANT_V>
+struct FixLdsT {
+    double ws[lp::ws_doubles_for<WANT_V>(B)];
     float D[B * B], S[B];
 };
+template <int B>
+using FixLds = FixLdsT<B, true>;
+template <int B>
+using FixLdsS = FixLdsT<B, false>;
 
 TMF_DEVI void block_of(uint32_t id, uint32_t per_frame, int nbw, int64_t &fr, int &bi, int &bj)
 {
@@ -160,7 +165,7 @@ TMF_DEVI void embed_fix_block(const EmbedArgs &a, uint32_t id, FixLds<B> &f, int
 }
 
 template <int B, class Par, int G>
-TMF_DEVI void extract_fix_block(const ExtractArgs &a, uint32_t id, FixLds<B> &f, int gl)
+TMF_DEVI void extract_fix_block(const ExtractArgs &a, uint32_t id, FixLdsS<B> &f, int gl)
 {
     const uint32_t per_frame = (uint32_t)a.nbh * (uint32_t)a.nbw;
     int64_t fr;
@@ -212,7 +217,7 @@ __global__ __launch_bounds__(64) void extract_fixup_kernel(ExtractArgs a, const 
 {
     constexpr int G = kFixLanes<B>, NG = 64 / G;
     static_assert(G >= B, "a group holds one element of dbdsqr's vectors per lane");
-    __shared__ FixLds<B> fl[NG];
+    __shared__ FixLdsS<B> fl[NG];
     const uint32_t n = *count;
     if (n <= gridDim.x) {
         if (blockIdx.x < n) extract_fix_block<B, lp::WavePar, 64>(a, list[blockIdx.x], fl[0], (int)threadIdx.x);

@@ -991,19 +991,23 @@ TMF_LPN void apply_pt(int n, double *A, const double *taup, double *VT, double *
 }
 
 // Working set of one block's dgesdd: A, U, VT (n x n), d, e, tauq, taup (n), and the BLAS /
-// dbdsqr work vectors (n + 4n) -- in doubles.  The fixup kernels carve it out of LDS.
+// dbdsqr work vectors (n + 4n) -- in doubles.  The fixup kernels carve it out of LDS.  Without
+// vectors (JOBZ = 'N', extract) U and VT are not part of it: A, then the vectors.
 TMF_LPI constexpr int ws_doubles(int n) { return 3 * n * n + 9 * n; }
+TMF_LPI constexpr int ws_doubles_s(int n) { return n * n + 9 * n; }
+template <bool WANT_V>
+TMF_LPI constexpr int ws_doubles_for(int n) { return WANT_V ? ws_doubles(n) : ws_doubles_s(n); }
 
 // np.linalg.svd of one float32 n x n block (row-major D): f32 U (row-major u[r][k]),
 // S, Vt (row-major vt[k][j]) exactly as numpy returns them, in the caller's workspace
-// ws (ws_doubles(n)).  Returns dbdsqr's info (0, or 1: not converged -- np.linalg.svd
+// ws (ws_doubles_for<WANT_V>(n)).  Returns dbdsqr's info (0, or 1: not converged -- np.linalg.svd
 // raises LinAlgError there).  Under WavePar every lane of the wave calls it for the same
 // block, with ws, D and the outputs in LDS or global memory visible to the whole wave.
 template <bool WANT_V, class P = SerialPar>
 TMF_LPN int svd_f32_ws(const float *D, int n, float *Uo, float *So, float *Vto, double *ws)
 {
-    double *A = ws, *U = A + n * n, *VT = U + n * n, *d = VT + n * n, *e = d + n, *tauq = e + n, *taup = tauq + n,
-           *work = taup + n;
+    double *A = ws, *U = WANT_V ? A + n * n : nullptr, *VT = WANT_V ? U + n * n : nullptr, *d = A + (WANT_V ? 3 : 1) * n * n,
+           *e = d + n, *tauq = e + n, *taup = tauq + n, *work = taup + n;
     LP_PAR(P, k, n * n) {
         const int j = k / n, i = k - j * n;
         A[i + j * n] = (double)D[i * n + j];
