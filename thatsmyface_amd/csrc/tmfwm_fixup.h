@@ -90,9 +90,28 @@ struct FixLdsT {
     float D[B * B], S[B];
 };
 template <int B>
-using FixLds = FixLdsT<B, true>;
-template <int B>
 using FixLdsS = FixLdsT<B, false>;
+// embed above b = 8: the DCT block D waits in the U slot of the workspace (the route copies it
+// into A before dbdsdc sets U to the identity) and the reconstruction M goes to the A slot (dead
+// after apply_pt): 1 KB less per b = 16 group, five waves per CU where four fitted -- the
+// reference route's embed<16> 1,882 -> 1,640 us per 1080p frame, while b = 8 measured 2 % slower
+// that way and keeps D and M apart (profiles/r04/r04m/ref_route_b{8,16}.log)
+template <int B>
+constexpr bool kFixAlias = B > 8;
+template <int B, bool ALIAS = kFixAlias<B>>
+struct FixLds {
+    double ws[lp::ws_doubles(B)];
+    float Dm[B * B], S[B];
+    TMF_DEVI float *D() { return Dm; }
+    TMF_DEVI float *M() { return Dm; }
+};
+template <int B>
+struct FixLds<B, true> {
+    double ws[lp::ws_doubles(B)];
+    float S[B];
+    TMF_DEVI float *D() { return reinterpret_cast<float *>(ws + B * B); }
+    TMF_DEVI float *M() { return reinterpret_cast<float *>(ws); }
+};
 
 TMF_DEVI void block_of(uint32_t id, uint32_t per_frame, int nbw, int64_t &fr, int &bi, int &bj)
 {
@@ -113,13 +132,13 @@ TMF_DEVI void embed_fix_block(const EmbedArgs &a, uint32_t id, FixLds<B> &f, int
     block_of(id, per_frame, a.nbw, fr, bi, bj);
     const uint8_t *src = a.src + fr * a.frame_stride;
     uint8_t *dst = a.dst + fr * a.frame_stride;
-    fix_load_dct<B, G>(src, a.W, bi, bj, f.D, gl);
-    const int info = lp::svd_f32_ws<true, Par>(f.D, runtime_n(B), nullptr, f.S, nullptr, f.ws);  // :195
+    fix_load_dct<B, G>(src, a.W, bi, bj, f.D(), gl);
+    const int info = lp::svd_f32_ws<true, Par>(f.D(), runtime_n(B), nullptr, f.S, nullptr, f.ws);  // :195
     if (info && gl == 0 && a.fb_bad) atomicAdd(a.fb_bad, 1u);
     // :198 blend, :201 U @ (diag(S) @ Vt) as OpenBLAS sgemm's fma chain over k, on U and Vt
     // rounded to f32 (numpy's astype) from the route's f64 U and VT
     const double *U64 = f.ws + B * B, *VT64 = f.ws + 2 * B * B;
-    float *M = f.D;
+    float *M = f.M();
     const double w = (double)a.wm[(int64_t)bi * a.nbw + bj];
     const float s0 = (float)((double)f.S[0] + a.alpha * (w / 255.0));
     for (int e = gl; e < B * B; e += G) {
