@@ -7,6 +7,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstring>
 #include <cstdlib>
 #include <vector>
 
@@ -56,6 +57,36 @@ static int run(int n, int kind, bool want_v)
     return info;
 }
 
+// The compact layout as the b > 8 embed pass uses it (tmfwm_fixup.h FixLds<B, true>): a workspace of
+// exactly ws_doubles_compact(n), D waiting in its U slot and S written into its e slot -- bounds
+// under ASan, and the same U, S, Vt bits as the standard layout.  Returns the mismatches (or 1000
+// when dbdsqr did not converge).
+template <class P>
+static int run_compact(int n, int kind)
+{
+    float *D = new float[n * n];
+    fill(D, n, kind);
+    float *U0 = new float[n * n], *V0 = new float[n * n], *S0 = new float[n], *U1 = new float[n * n], *V1 = new float[n * n];
+    double *ws0 = new double[ws_doubles(n)];
+    const int i0 = svd_f32_ws<true, P>(D, n, U0, S0, V0, ws0);
+    double *ws = new double[ws_doubles_compact(n)];
+    float *Din = reinterpret_cast<float *>(ws + n * n), *S1 = reinterpret_cast<float *>(ws + 3 * n * n + n);
+    for (int k = 0; k < n * n; ++k) Din[k] = D[k];
+    const int i1 = svd_f32_ws<true, P, true>(Din, n, U1, S1, V1, ws);
+    int bad = (i0 || i1) ? 1000 : 0;
+    for (int k = 0; k < n * n; ++k) bad += (std::memcmp(&U0[k], &U1[k], 4) != 0) + (std::memcmp(&V0[k], &V1[k], 4) != 0);
+    for (int k = 0; k < n; ++k) bad += std::memcmp(&S0[k], &S1[k], 4) != 0;
+    delete[] ws;
+    delete[] ws0;
+    delete[] V1;
+    delete[] U1;
+    delete[] S0;
+    delete[] V0;
+    delete[] U0;
+    delete[] D;
+    return bad;
+}
+
 int main()
 {
     int cases = 0, bad = 0;
@@ -67,6 +98,13 @@ int main()
                     bad += run<ReversePar>(n, kind, v) != 0;
                     cases += 2;
                 }
-    std::printf("{\"cases\": %d, \"not_converged\": %d}\n", cases, bad);
+    int compact_cases = 0, compact_bad = 0;
+    for (int n = 1; n <= kMaxN; ++n)
+        for (int kind = 0; kind < 8; ++kind) {
+            compact_bad += run_compact<SerialPar>(n, kind) + run_compact<ReversePar>(n, kind);
+            compact_cases += 2;
+        }
+    std::printf("{\"cases\": %d, \"not_converged\": %d, \"compact_cases\": %d, \"compact_mismatches\": %d}\n", cases, bad,
+                compact_cases, compact_bad);
     return 0;
 }

@@ -97,3 +97,5 @@ def test_workspace_bounds_asan(tmp_path):
                        env=dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=1"))
     assert r.returncode == 0, r.stderr[-3000:]
     assert '"cases": 2048' in r.stdout and '"not_converged": 0' in r.stdout, r.stdout
+    # the compact workspace of the b > 8 embed pass: in bounds, same bits as the standard layout
+    assert '"compact_cases": 256' in r.stdout and '"compact_mismatches": 0' in r.stdout, r.stdout

@@ -91,26 +91,29 @@ struct FixLdsT {
 };
 template <int B>
 using FixLdsS = FixLdsT<B, false>;
-// embed above b = 8: the DCT block D waits in the U slot of the workspace (the route copies it
-// into A before dbdsdc sets U to the identity) and the reconstruction M goes to the A slot (dead
-// after apply_pt): 1 KB less per b = 16 group, five waves per CU where four fitted -- the
-// reference route's embed<16> 1,882 -> 1,640 us per 1080p frame, while b = 8 measured 2 % slower
-// that way and keeps D and M apart (profiles/r04/r04m/ref_route_b{8,16}.log)
+// embed above b = 8: the compact workspace (lp::ws_doubles_compact: no work slot) with the DCT
+// block D waiting in the U slot (the route copies it into A before anything else writes there),
+// the reconstruction M in the A slot (dead after apply_pt) and S in the e slot (e is in
+// registers by then): 7.4 -> 6.5 KB per b = 16 group, six waves per CU where four fitted; b = 8
+// measured 2 % slower with D and M inside its workspace and keeps them apart
 template <int B>
 constexpr bool kFixAlias = B > 8;
 template <int B, bool ALIAS = kFixAlias<B>>
 struct FixLds {
+    static constexpr bool kCompact = false;
     double ws[lp::ws_doubles(B)];
-    float Dm[B * B], S[B];
+    float Dm[B * B], Sv[B];
     TMF_DEVI float *D() { return Dm; }
     TMF_DEVI float *M() { return Dm; }
+    TMF_DEVI float *S() { return Sv; }
 };
 template <int B>
 struct FixLds<B, true> {
-    double ws[lp::ws_doubles(B)];
-    float S[B];
+    static constexpr bool kCompact = true;
+    double ws[lp::ws_doubles_compact(B)];
     TMF_DEVI float *D() { return reinterpret_cast<float *>(ws + B * B); }
     TMF_DEVI float *M() { return reinterpret_cast<float *>(ws); }
+    TMF_DEVI float *S() { return reinterpret_cast<float *>(ws + 3 * B * B + B); }
 };
 
 TMF_DEVI void block_of(uint32_t id, uint32_t per_frame, int nbw, int64_t &fr, int &bi, int &bj)
@@ -133,20 +136,21 @@ TMF_DEVI void embed_fix_block(const EmbedArgs &a, uint32_t id, FixLds<B> &f, int
     const uint8_t *src = a.src + fr * a.frame_stride;
     uint8_t *dst = a.dst + fr * a.frame_stride;
     fix_load_dct<B, G>(src, a.W, bi, bj, f.D(), gl);
-    const int info = lp::svd_f32_ws<true, Par>(f.D(), runtime_n(B), nullptr, f.S, nullptr, f.ws);  // :195
+    float *S = f.S();
+    const int info = lp::svd_f32_ws<true, Par, FixLds<B>::kCompact>(f.D(), runtime_n(B), nullptr, S, nullptr, f.ws);  // :195
     if (info && gl == 0 && a.fb_bad) atomicAdd(a.fb_bad, 1u);
     // :198 blend, :201 U @ (diag(S) @ Vt) as OpenBLAS sgemm's fma chain over k, on U and Vt
     // rounded to f32 (numpy's astype) from the route's f64 U and VT
     const double *U64 = f.ws + B * B, *VT64 = f.ws + 2 * B * B;
     float *M = f.M();
     const double w = (double)a.wm[(int64_t)bi * a.nbw + bj];
-    const float s0 = (float)((double)f.S[0] + a.alpha * (w / 255.0));
+    const float s0 = (float)((double)S[0] + a.alpha * (w / 255.0));
     for (int e = gl; e < B * B; e += G) {
         const int i = e / B, j = e % B;
         float acc = 0.0f;
 #pragma unroll
         for (int k = 0; k < B; ++k)
-            acc = __builtin_fmaf((float)U64[i + k * B], (k == 0 ? s0 : f.S[k]) * (float)VT64[k + j * B], acc);
+            acc = __builtin_fmaf((float)U64[i + k * B], (k == 0 ? s0 : S[k]) * (float)VT64[k + j * B], acc);
         M[e] = acc;
     }
     group_sync();

@@ -995,6 +995,10 @@ TMF_LPN void apply_pt(int n, double *A, const double *taup, double *VT, double *
 // vectors (JOBZ = 'N', extract) U and VT are not part of it: A, then the vectors.
 TMF_LPI constexpr int ws_doubles(int n) { return 3 * n * n + 9 * n; }
 TMF_LPI constexpr int ws_doubles_s(int n) { return n * n + 9 * n; }
+// the compact layout (svd_f32_ws<true, P, true>): no work slot of its own -- dgebd2's dlarf vector
+// sits in U's slot (free until dbdsdc sets U to the identity), apply_q / apply_pt's in d's (d and
+// e are in registers by then) -- so A, U, VT, d, e, tauq, taup: 3 n^2 + 4 n
+TMF_LPI constexpr int ws_doubles_compact(int n) { return 3 * n * n + 4 * n; }
 template <bool WANT_V>
 TMF_LPI constexpr int ws_doubles_for(int n) { return WANT_V ? ws_doubles(n) : ws_doubles_s(n); }
 
@@ -1003,11 +1007,12 @@ TMF_LPI constexpr int ws_doubles_for(int n) { return WANT_V ? ws_doubles(n) : ws
 // ws (ws_doubles_for<WANT_V>(n)).  Returns dbdsqr's info (0, or 1: not converged -- np.linalg.svd
 // raises LinAlgError there).  Under WavePar every lane of the wave calls it for the same
 // block, with ws, D and the outputs in LDS or global memory visible to the whole wave.
-template <bool WANT_V, class P = SerialPar>
+template <bool WANT_V, class P = SerialPar, bool COMPACT = false>
 TMF_LPN int svd_f32_ws(const float *D, int n, float *Uo, float *So, float *Vto, double *ws)
 {
+    static_assert(!COMPACT || WANT_V, "the compact layout borrows U's slot");
     double *A = ws, *U = WANT_V ? A + n * n : nullptr, *VT = WANT_V ? U + n * n : nullptr, *d = A + (WANT_V ? 3 : 1) * n * n,
-           *e = d + n, *tauq = e + n, *taup = tauq + n, *work = taup + n;
+           *e = d + n, *tauq = e + n, *taup = tauq + n, *work = COMPACT ? U : taup + n;
     LP_PAR(P, k, n * n) {
         const int j = k / n, i = k - j * n;
         A[i + j * n] = (double)D[i * n + j];
@@ -1020,8 +1025,9 @@ TMF_LPN int svd_f32_ws(const float *D, int n, float *Uo, float *So, float *Vto, 
     ev.load(e, n - 1);
     const int info = dbdsdc<WANT_V, P>(n, dv, ev, U, n, VT, n);
     if (WANT_V) {
-        apply_q<P>(n, A, tauq, U, work);
-        apply_pt<P>(n, A, taup, VT, work);
+        double *work2 = COMPACT ? d : work;
+        apply_q<P>(n, A, tauq, U, work2);
+        apply_pt<P>(n, A, taup, VT, work2);
         if (Uo) {  // NULL: the caller reads U (ws + n^2) and VT (ws + 2 n^2), column-major f64, itself
             LP_PAR(P, q, n * n) {
                 const int i = q / n, k = q - i * n;
