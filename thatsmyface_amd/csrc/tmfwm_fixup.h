@@ -94,10 +94,11 @@ using FixLdsS = FixLdsT<B, false>;
 // embed above b = 8: the compact workspace (lp::ws_doubles_compact: no work slot) with the DCT
 // block D waiting in the U slot (the route copies it into A before anything else writes there),
 // the reconstruction M in the A slot (dead after apply_pt) and S in the e slot (e is in
-// registers by then): 7.4 -> 6.5 KB per b = 16 group, six waves per CU where four fitted; b = 8
-// measured 2 % slower with D and M inside its workspace and keeps them apart
+// registers by then): 8.4 -> 6.5 KB per b = 16 group, six waves per CU where four fitted
+// (embed<16> -24 %, <12> -6 %, <8> -3 %; b = 6 +-0.5 % keeps the standard layout,
+// profiles/r04/r04n/, r04o/)
 template <int B>
-constexpr bool kFixAlias = B > 8;
+constexpr bool kFixAlias = B >= 8;
 template <int B, bool ALIAS = kFixAlias<B>>
 struct FixLds {
     static constexpr bool kCompact = false;
