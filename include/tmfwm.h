@@ -188,6 +188,15 @@ int tmfwm_extract_multi(const uint8_t *wm_rgb, const uint8_t *orig_rgb, int64_t 
                         int64_t frame_stride, int32_t block, double alpha, uint8_t *out_tiles, const int32_t *devices,
                         int32_t n_shards, int64_t *n_lapack_blocks);
 
+/* The multi-GPU calls with an explicit SVD route (ABI 8; TMFWM_ROUTE_*, as tmfwm_embed_route):
+ * tmfwm_embed_multi / tmfwm_extract_multi are these with TMFWM_ROUTE_HYBRID. */
+int tmfwm_embed_multi_route(const uint8_t *rgb, int64_t n_frames, int32_t height, int32_t width, int64_t frame_stride,
+                            const uint8_t *wm_tile, int32_t block, double alpha, uint8_t *out, const int32_t *devices,
+                            int32_t n_shards, int32_t route, int64_t *n_lapack_blocks);
+int tmfwm_extract_multi_route(const uint8_t *wm_rgb, const uint8_t *orig_rgb, int64_t n_frames, int32_t height, int32_t width,
+                              int64_t frame_stride, int32_t block, double alpha, uint8_t *out_tiles, const int32_t *devices,
+                              int32_t n_shards, int32_t route, int64_t *n_lapack_blocks);
+
 /* rgb_to_ycbcr (watermarking.py:23): npix RGB uint8 pixels -> npix x 3 float32 (Y, Cb+0.5, Cr+0.5). */
 int tmfwm_rgb_to_ycbcr(const uint8_t *rgb, int64_t npix, float *ycc, int32_t mem_kind, void *hip_stream);
 

@@ -128,6 +128,11 @@ def test_multi_entry_points_validate_then_need_a_device():
         multi.embed_multi(a, np.zeros((3, 3), np.uint8), 8, 0.1)
     L = _lib.load()
     p = lambda x: x.ctypes.data  # noqa: E731
+    with pytest.raises(ValueError, match="route"):
+        multi.embed_multi(a, t, 8, 0.1, route="exact")
+    with pytest.raises(ValueError, match="route"):
+        _lib.check(_lib.load().tmfwm_embed_multi_route(a.ctypes.data, 2, 16, 16, 16 * 16 * 3, t.ctypes.data, 8, 0.1, a.ctypes.data,
+                                                       None, 0, 2, None), "embed_multi_route")
     with pytest.raises(ValueError):  # alpha = 0 divides by zero in extract (watermarking.py:285)
         _lib.check(L.tmfwm_extract_multi(p(a), p(a), 2, 16, 16, 16 * 16 * 3, 8, 0.0, p(t), None, 0, None), "extract_multi")
     if _lib.device_count() == 0:

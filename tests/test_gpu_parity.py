@@ -947,3 +947,23 @@ def test_dropin_zero_copy_pil_path(dev, monkeypatch):
     gc.collect()
     c = W.embed_watermark(cover, wm, False, cfg)
     assert c._tmfwm_rgbx.ctypes.data == buf and np.array_equal(np.asarray(c), np.asarray(a))
+
+
+def test_multi_entry_points_reference_route(dev):
+    """tmfwm_embed_multi_route / tmfwm_extract_multi_route (ABI 8) on the reference route, two
+    logical shards on device 0: the oracle's dgesdd route for every frame, and every block counted."""
+    from lapack_path import photo_cover
+
+    from thatsmyface_amd import multi
+
+    b, H, W, n = 8, 72, 112, 3
+    host = np.stack([photo_cover(H, W, 60 + i) for i in range(n)])
+    t = _u8(61, (H // b, W // b))
+    st, xs = {}, {}
+    out = multi.embed_multi(host, t, b, 0.1, devices=[0, 0], stats=st, route="reference")
+    ext = multi.extract_multi(out, host, b, 0.1, devices=[0, 0], stats=xs, route="reference")
+    assert st["lapack_blocks"] == xs["lapack_blocks"] == n * (H // b) * (W // b)
+    for f in range(n):
+        ref = O.embed_frame(host[f], t, b, 0.1, route="lapack")
+        assert np.array_equal(out[f], ref), f
+        assert np.array_equal(ext[f], O.extract_frame(ref, host[f], b, 0.1, route="lapack")), f

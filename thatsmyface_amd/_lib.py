@@ -73,6 +73,8 @@ SIGNATURES = {
     "tmfwm_extract_px": (ctypes.c_int, [_VP, _I32, _I64, _VP, _I32, _I64, _I64, _I32, _I32, _I32, _D, _VP, _I32, _VP, _I32, _VP]),
     "tmfwm_embed_multi": (ctypes.c_int, [_VP, _I64, _I32, _I32, _I64, _VP, _I32, _D, _VP, _VP, _I32, _VP]),
     "tmfwm_extract_multi": (ctypes.c_int, [_VP, _VP, _I64, _I32, _I32, _I64, _I32, _D, _VP, _VP, _I32, _VP]),
+    "tmfwm_embed_multi_route": (ctypes.c_int, [_VP, _I64, _I32, _I32, _I64, _VP, _I32, _D, _VP, _VP, _I32, _I32, _VP]),
+    "tmfwm_extract_multi_route": (ctypes.c_int, [_VP, _VP, _I64, _I32, _I32, _I64, _I32, _D, _VP, _VP, _I32, _I32, _VP]),
     "tmfwm_rgb_to_ycbcr": (ctypes.c_int, [_VP, _I64, _VP, _I32, _VP]),
     "tmfwm_ycbcr_to_rgb": (ctypes.c_int, [_VP, _I64, _VP, _I32, _VP]),
     "tmfwm_rgb_to_ycbcr_f32": (ctypes.c_int, [_VP, _I64, _VP, _I32, _VP]),

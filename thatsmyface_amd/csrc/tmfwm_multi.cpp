@@ -408,12 +408,13 @@ int make_streams(std::vector<Shard> &sh)
 
 extern "C" {
 
-int tmfwm_embed_multi(const uint8_t *rgb, int64_t n_frames, int32_t height, int32_t width, int64_t frame_stride,
-                      const uint8_t *wm_tile, int32_t block, double alpha, uint8_t *out, const int32_t *devices,
-                      int32_t n_shards, int64_t *n_lapack_blocks)
+int tmfwm_embed_multi_route(const uint8_t *rgb, int64_t n_frames, int32_t height, int32_t width, int64_t frame_stride,
+                            const uint8_t *wm_tile, int32_t block, double alpha, uint8_t *out, const int32_t *devices,
+                            int32_t n_shards, int32_t route, int64_t *n_lapack_blocks)
 {
     tmf::clear_error();
     if (n_lapack_blocks) *n_lapack_blocks = 0;
+    if (route != TMFWM_ROUTE_HYBRID && route != TMFWM_ROUTE_REFERENCE) return report(TMFWM_ERR_INVALID, "route %d", route);
     if (int rc = tmf::check_frames(n_frames, height, width, frame_stride, block)) return rc;
     if (!std::isfinite(alpha)) return report(TMFWM_ERR_INVALID, "alpha is not finite");
     const int nbh = height / block, nbw = width / block;
@@ -446,7 +447,7 @@ int tmfwm_embed_multi(const uint8_t *rgb, int64_t n_frames, int32_t height, int3
                     return 0;
                 },
                 [&](int64_t k, const uint8_t *din, int64_t, uint8_t *dout, hipStream_t st, uint32_t *sink) -> int {
-                    return tmf::embed_device_async(din, k, height, width, fbytes, u.tile, block, alpha, dout, st, sink);
+                    return tmf::embed_device_async(din, k, height, width, fbytes, u.tile, block, alpha, dout, st, sink, route);
                 },
                 [&](int64_t f, int64_t k, const uint8_t *dout, hipStream_t st) -> int {
                     if (frame_stride == fbytes)
@@ -463,12 +464,13 @@ int tmfwm_embed_multi(const uint8_t *rgb, int64_t n_frames, int32_t height, int3
     return join(sh, th, n_lapack_blocks);
 }
 
-int tmfwm_extract_multi(const uint8_t *wm_rgb, const uint8_t *orig_rgb, int64_t n_frames, int32_t height, int32_t width,
-                        int64_t frame_stride, int32_t block, double alpha, uint8_t *out_tiles, const int32_t *devices,
-                        int32_t n_shards, int64_t *n_lapack_blocks)
+int tmfwm_extract_multi_route(const uint8_t *wm_rgb, const uint8_t *orig_rgb, int64_t n_frames, int32_t height, int32_t width,
+                              int64_t frame_stride, int32_t block, double alpha, uint8_t *out_tiles, const int32_t *devices,
+                              int32_t n_shards, int32_t route, int64_t *n_lapack_blocks)
 {
     tmf::clear_error();
     if (n_lapack_blocks) *n_lapack_blocks = 0;
+    if (route != TMFWM_ROUTE_HYBRID && route != TMFWM_ROUTE_REFERENCE) return report(TMFWM_ERR_INVALID, "route %d", route);
     if (int rc = tmf::check_frames(n_frames, height, width, frame_stride, block)) return rc;
     if (!std::isfinite(alpha) || alpha == 0.0) return report(TMFWM_ERR_INVALID, "alpha must be finite and non-zero");
     const int64_t tbytes = (int64_t)(height / block) * (width / block);
@@ -498,7 +500,8 @@ int tmfwm_extract_multi(const uint8_t *wm_rgb, const uint8_t *orig_rgb, int64_t 
                     return 0;
                 },
                 [&](int64_t k, const uint8_t *din, int64_t half, uint8_t *dout, hipStream_t st, uint32_t *sink) -> int {
-                    return tmf::extract_device_async(din, din + half, k, height, width, fbytes, block, alpha, dout, st, sink);
+                    return tmf::extract_device_async(din, din + half, k, height, width, fbytes, block, alpha, dout, st, sink,
+                                                     route);
                 },
                 [&](int64_t f, int64_t k, const uint8_t *dout, hipStream_t st) -> int {
                     return hipMemcpyAsync(out_tiles + f * tbytes, dout, (size_t)(k * tbytes), hipMemcpyDeviceToHost, st) == hipSuccess
@@ -507,6 +510,22 @@ int tmfwm_extract_multi(const uint8_t *wm_rgb, const uint8_t *orig_rgb, int64_t 
         });
     }
     return join(sh, th, n_lapack_blocks);
+}
+
+int tmfwm_embed_multi(const uint8_t *rgb, int64_t n_frames, int32_t height, int32_t width, int64_t frame_stride,
+                      const uint8_t *wm_tile, int32_t block, double alpha, uint8_t *out, const int32_t *devices,
+                      int32_t n_shards, int64_t *n_lapack_blocks)
+{
+    return tmfwm_embed_multi_route(rgb, n_frames, height, width, frame_stride, wm_tile, block, alpha, out, devices, n_shards,
+                                   TMFWM_ROUTE_HYBRID, n_lapack_blocks);
+}
+
+int tmfwm_extract_multi(const uint8_t *wm_rgb, const uint8_t *orig_rgb, int64_t n_frames, int32_t height, int32_t width,
+                        int64_t frame_stride, int32_t block, double alpha, uint8_t *out_tiles, const int32_t *devices,
+                        int32_t n_shards, int64_t *n_lapack_blocks)
+{
+    return tmfwm_extract_multi_route(wm_rgb, orig_rgb, n_frames, height, width, frame_stride, block, alpha, out_tiles, devices,
+                                     n_shards, TMFWM_ROUTE_HYBRID, n_lapack_blocks);
 }
 
 }  // extern "C"

@@ -31,9 +31,10 @@ def _device_list(devices):
 
 
 def embed_multi(frames: np.ndarray, wm_tile: np.ndarray, block: int = 8, alpha: float = 0.1, devices=None,
-                stats: dict | None = None) -> np.ndarray:
+                stats: dict | None = None, route: str = "hybrid") -> np.ndarray:
     """Embed one tile into every frame, frames sharded over `devices` (default: every
-    visible GPU; repeat a device for logical shards).  stats receives "lapack_blocks"."""
+    visible GPU; repeat a device for logical shards).  stats receives "lapack_blocks";
+    route as batch.embed_batch ("hybrid" or "reference")."""
     frames = _frames(frames, "frames")
     n, h, w, _ = frames.shape
     if block not in SUPPORTED_BLOCK_SIZES:
@@ -45,15 +46,15 @@ def embed_multi(frames: np.ndarray, wm_tile: np.ndarray, block: int = 8, alpha: 
     devs, k = _device_list(devices)
     cnt = ctypes.c_int64(0)
     L = _lib.load()
-    _lib.check(L.tmfwm_embed_multi(frames.ctypes.data, n, h, w, h * w * 3, tile.ctypes.data, block, float(alpha),
-                                   out.ctypes.data, devs, k, ctypes.addressof(cnt)), "embed_multi")
+    _lib.check(L.tmfwm_embed_multi_route(frames.ctypes.data, n, h, w, h * w * 3, tile.ctypes.data, block, float(alpha),
+                                         out.ctypes.data, devs, k, _lib.route_code(route), ctypes.addressof(cnt)), "embed_multi")
     if stats is not None:
         stats["lapack_blocks"] = int(cnt.value)
     return out
 
 
 def extract_multi(wframes: np.ndarray, oframes: np.ndarray, block: int = 8, alpha: float = 0.1, devices=None,
-                  stats: dict | None = None) -> np.ndarray:
+                  stats: dict | None = None, route: str = "hybrid") -> np.ndarray:
     """Extract every frame pair's tile, pairs sharded over `devices`."""
     wframes = _frames(wframes, "wframes")
     oframes = _frames(oframes, "oframes")
@@ -66,8 +67,9 @@ def extract_multi(wframes: np.ndarray, oframes: np.ndarray, block: int = 8, alph
     devs, k = _device_list(devices)
     cnt = ctypes.c_int64(0)
     L = _lib.load()
-    _lib.check(L.tmfwm_extract_multi(wframes.ctypes.data, oframes.ctypes.data, n, h, w, h * w * 3, block, float(alpha),
-                                     out.ctypes.data, devs, k, ctypes.addressof(cnt)), "extract_multi")
+    _lib.check(L.tmfwm_extract_multi_route(wframes.ctypes.data, oframes.ctypes.data, n, h, w, h * w * 3, block, float(alpha),
+                                           out.ctypes.data, devs, k, _lib.route_code(route), ctypes.addressof(cnt)),
+               "extract_multi")
     if stats is not None:
         stats["lapack_blocks"] = int(cnt.value)
     return out
