@@ -64,3 +64,39 @@ def test_module_path_shim():
 
     assert watermarking.embed_watermark is W.embed_watermark
     assert constants.BLOCK_SIZE == 8 and constants.ALPHA == 0.1
+
+
+def test_zero_copy_pil_helpers():
+    """Host side of the drop-in's zero-copy PIL path, no GPU needed: PIL's own
+    4-byte memory of a single-block RGB image is handed over (its bytes are the pixels plus a
+    pad byte), read-only and multi-block images are not, embed_watermark's own outputs hand over
+    their buffer while PIL has not copied them, and pooled buffers come back only once nothing
+    references them."""
+    import gc
+
+    pytest.importorskip("pyarrow")
+    if not W._zero_copy:
+        pytest.skip("TMFWM_PIL_ZERO_COPY=0")
+    rng = np.random.default_rng(5)
+    arr = rng.integers(0, 256, (48, 80, 3), dtype=np.uint8)
+    img = Image.fromarray(arr)
+    addr, keep = W._rgbx_view(img)
+    import ctypes
+
+    got = np.frombuffer((ctypes.c_uint8 * (48 * 80 * 4)).from_address(addr), np.uint8).reshape(48, 80, 4)
+    assert np.array_equal(got[..., :3], arr)
+    del keep
+    assert W._rgbx_view(Image.new("RGB", (3840, 2160))) is None  # several memory blocks
+    # an output buffer wrapped as an RGB image: same pixels, read-only, its buffer handed back
+    buf = W._take_out(48 * 80 * 4)
+    buf.reshape(48, 80, 4)[..., :3] = arr
+    out = W._rgb_from_rgbx(buf, 80, 48)
+    assert out.mode == "RGB" and out.readonly and np.array_equal(np.asarray(out), arr)
+    assert W._rgbx_view(out)[0] == buf.ctypes.data
+    assert W._take_out(48 * 80 * 4) is not buf  # still referenced by the image
+    out.paste((1, 2, 3), (0, 0, 4, 4))  # PIL copies first: the buffer is no longer the image's
+    assert not out.readonly and W._rgbx_view(out)[0] != buf.ctypes.data
+    where = buf.ctypes.data
+    del out, buf  # the pool counts every reference, this test's own included
+    gc.collect()
+    assert W._take_out(48 * 80 * 4).ctypes.data == where
