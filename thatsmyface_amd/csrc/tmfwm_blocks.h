@@ -193,7 +193,6 @@ constexpr int kEmbedWaves = (B == 12 || B == 16) ? 2 : 1;
 // waves keep going as before.
 template <int B>
 constexpr int kDeferMax = B == 8 ? 4 : 0;
-constexpr unsigned kListPassGrid = 2048;  // waves of the list pass (2 per SIMD fill the chip)
 
 // b = 16 parks D in LDS during phase 1 (svd3, PARK): frees 32 VGPRs (scratch 264 -> 216 B
 // per lane); at b = 10 / 14 the allocation without it fits 2 waves per SIMD spill-free and
@@ -239,7 +238,11 @@ TMF_DEVI void embed_blocks(const EmbedArgs &a, const StripPos &pos, uint32_t id,
     static_assert(!kPark || kParkOff<L> + B * B <= TS, "parked D fits the tile");
     bool slow = false;  // strip pass: this block was left to the list pass
     svd3<B, L, kPark>(x, A, V, q, stamp, tile, tile + kParkOff<L>, !LIST && a.slow_list ? kDeferMax<B> : 0, &slow);
-    if (slow && pos.valid && q == 0) a.slow_list[atomicAdd(a.slow_count, 1u)] = id;
+    if (slow && pos.valid && q == 0) {
+        const uint32_t row = blockIdx.y * (uint32_t)a.nbh + (uint32_t)pos.bi, s = row % kListShards;
+        a.slow_list[shard_base(s, (uint32_t)a.nframes * (uint32_t)a.nbh, (uint32_t)a.nbw) +
+                    atomicAdd(a.slow_shards + s * kShardStride, 1u)] = id;
+    }
 
     // singular values, U = A / sigma, sort descending (oracle orc_svd_block)
     double sig[B];
@@ -395,19 +398,23 @@ __global__ __launch_bounds__(64, kEmbedWaves<B>) void embed_kernel(EmbedArgs a)
     __shared__ __attribute__((aligned(16))) float lds[BPW * TS];  // also svd3's scratch during the SVD
     __shared__ uint32_t pix[R * NW][64];  // this lane's source bytes, parked during the SVD
     if constexpr (LIST) {
-        // grid-stride over the slow list (its length is known on the device only)
-        const uint32_t n = *a.slow_count, per_frame = (uint32_t)a.nbh * (uint32_t)a.nbw;
+        // grid-stride over the slow list's segments (their lengths are known on the device only)
+        const uint32_t per_frame = (uint32_t)a.nbh * (uint32_t)a.nbw, rows = (uint32_t)a.nframes * (uint32_t)a.nbh;
         const int g = (threadIdx.x & 63) / L;
-        for (uint32_t t0 = blockIdx.x * BPW; t0 < n; t0 += gridDim.x * BPW) {
-            StripPos pos;
-            pos.valid = t0 + g < n;
-            const uint32_t id = pos.valid ? a.slow_list[t0 + g] : 0u;
-            pos.frame = id / per_frame;
-            const uint32_t rem = id % per_frame;
-            pos.bi = (int)(rem / (uint32_t)a.nbw);
-            pos.bj = (int)(rem % (uint32_t)a.nbw);
-            embed_blocks<B, true>(a, pos, id, lds, pix);
-            __syncthreads();  // the LDS tiles are reused by the next listed blocks
+        for (uint32_t s = blockIdx.x; s < kListShards; s += gridDim.x) {
+            const uint32_t n = a.slow_shards[s * kShardStride], base = shard_base(s, rows, (uint32_t)a.nbw);
+            if (n != 0 && (threadIdx.x & 63) == 0) atomicAdd(a.slow_count, n);
+            for (uint32_t t0 = 0; t0 < n; t0 += BPW) {
+                StripPos pos;
+                pos.valid = t0 + g < n;
+                const uint32_t id = pos.valid ? a.slow_list[base + t0 + g] : 0u;
+                pos.frame = id / per_frame;
+                const uint32_t rem = id % per_frame;
+                pos.bi = (int)(rem / (uint32_t)a.nbw);
+                pos.bj = (int)(rem % (uint32_t)a.nbw);
+                embed_blocks<B, true>(a, pos, id, lds, pix);
+                __syncthreads();  // the LDS tiles are reused by the next listed blocks
+            }
         }
     } else {
         const StripPos pos = strip_pos<B>(a.strips_per_row, a.nbw);

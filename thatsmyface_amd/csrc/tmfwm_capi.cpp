@@ -291,11 +291,13 @@ int run_embed(EmbedArgs a, hipStream_t st, int64_t *n_lapack, bool check, uint32
 {
     Chunks ch;
     ch.plan(a.nframes, (int64_t)a.nbh * a.nbw);
-    DevBuf list, slow, counts;
+    DevBuf list, slow, shards, counts;
     if (ch.cap > 0) {
         if (int rc = list.alloc((size_t)ch.cap * 4, st, "dgesdd-route block list")) return rc;
-        if (embed_defers(a.block) && route == TMFWM_ROUTE_HYBRID)
+        if (embed_defers(a.block) && route == TMFWM_ROUTE_HYBRID) {
             if (int rc = slow.alloc((size_t)ch.cap * 4, st, "list-pass block list")) return rc;
+            if (int rc = shards.alloc((size_t)kListShards * kShardStride * 4, st, "list-pass segment counters")) return rc;
+        }
         // per chunk: dgesdd-route count, non-convergence count, list-pass count
         if (int rc = counts.alloc((size_t)ch.n * 12, st, "block-list counts")) return rc;
         TMF_HIP(hipMemsetAsync(counts.p, 0, (size_t)ch.n * 12, st));
@@ -320,6 +322,8 @@ int run_embed(EmbedArgs a, hipStream_t st, int64_t *n_lapack, bool check, uint32
         k.fb_bad = static_cast<uint32_t *>(counts.p) + ch.n + c;
         k.slow_list = static_cast<uint32_t *>(slow.p);  // null unless embed_defers(block)
         k.slow_count = static_cast<uint32_t *>(counts.p) + 2 * ch.n + c;
+        k.slow_shards = static_cast<uint32_t *>(shards.p);
+        if (shards.p) TMF_HIP(hipMemsetAsync(shards.p, 0, (size_t)kListShards * kShardStride * 4, st));
         if (route == TMFWM_ROUTE_REFERENCE) {  // every block on the dgesdd route; the edges as always
             TMF_HIP(launch_edges(k.src, k.dst, k.nframes, k.H, k.W, k.frame_stride, k.block, st));
             TMF_HIP(launch_list_all(k.fb_list, k.fb_count, k.nframes * ch.per_frame, st));
@@ -350,10 +354,12 @@ int run_extract(ExtractArgs a, hipStream_t st, int64_t *n_lapack, bool check, ui
         }
         return 0;
     }
-    DevBuf list, slow, counts;
+    DevBuf list, slow, shards, counts;
     if (int rc = list.alloc((size_t)ch.cap * 4, st, "dgesdd-route block list")) return rc;
-    if (route == TMFWM_ROUTE_HYBRID)
+    if (route == TMFWM_ROUTE_HYBRID) {
         if (int rc = slow.alloc((size_t)ch.cap * 4, st, "list-pass block list")) return rc;
+        if (int rc = shards.alloc((size_t)kListShards * kShardStride * 4, st, "list-pass segment counters")) return rc;
+    }
     if (int rc = counts.alloc((size_t)ch.n * 12, st, "block-list counts")) return rc;  // as run_embed's
     TMF_HIP(hipMemsetAsync(counts.p, 0, (size_t)ch.n * 12, st));
     for (int64_t c = 0; c < ch.n; ++c) {
@@ -368,6 +374,8 @@ int run_extract(ExtractArgs a, hipStream_t st, int64_t *n_lapack, bool check, ui
         k.fb_bad = static_cast<uint32_t *>(counts.p) + ch.n + c;
         k.slow_list = static_cast<uint32_t *>(slow.p);
         k.slow_count = static_cast<uint32_t *>(counts.p) + 2 * ch.n + c;
+        k.slow_shards = static_cast<uint32_t *>(shards.p);
+        if (shards.p) TMF_HIP(hipMemsetAsync(shards.p, 0, (size_t)kListShards * kShardStride * 4, st));
         if (route == TMFWM_ROUTE_REFERENCE) TMF_HIP(launch_list_all(k.fb_list, k.fb_count, k.nframes * ch.per_frame, st));
         else TMF_HIP(launch_extract(k, st));
         TMF_HIP(launch_extract_fixup(k, k.fb_list, k.fb_count, k.nframes * ch.per_frame, st));

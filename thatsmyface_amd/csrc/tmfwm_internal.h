@@ -9,6 +9,18 @@
 
 namespace tmf {
 
+// One append counter per segment instead of one per launch: at b = 4 most strip-pass waves
+// append, and device-scope atomics on one address serialise.
+constexpr uint32_t kListShards = 2048, kShardStride = 16;  // counters 64 bytes apart
+
+// first slot of segment s when rows block rows of nbw blocks are dealt round-robin over
+// kListShards segments (segment s holds rows s, s + kListShards, ...; exact capacity)
+__host__ __device__ inline uint32_t shard_base(uint32_t s, uint32_t rows, uint32_t nbw)
+{
+    const uint32_t q = rows / kListShards, r = rows % kListShards;
+    return (uint32_t)(((uint64_t)s * q + (s < r ? s : r)) * nbw);
+}
+
 struct EmbedArgs {
     const uint8_t *src;
     uint8_t *dst;
@@ -24,9 +36,11 @@ struct EmbedArgs {
     uint32_t *fb_count;
     uint32_t *fb_bad;        // dgesdd-route blocks whose dbdsqr did not converge (may be null)
     // list pass: blocks the first pass leaves unfinished after its f64 sweep
-    // budget, same ids; null: the first pass runs every block to the end
+    // budget, same ids; null: the first pass runs every block to the end.  Segmented as
+    // ExtractArgs' list (kListShards, shard_base, slow_shards)
     uint32_t *slow_list;
     uint32_t *slow_count;
+    uint32_t *slow_shards;
 };
 
 struct ExtractArgs {
@@ -43,9 +57,13 @@ struct ExtractArgs {
     uint32_t *fb_count;
     uint32_t *fb_bad;        // dgesdd-route blocks whose dbdsqr did not converge (may be null)
     // list pass: blocks the strip pass's power iterations left undecided, redone
-    // with more iterations before the dgesdd route; null: straight to the dgesdd route
+    // with more iterations before the dgesdd route; null: straight to the dgesdd route.  The
+    // list is kListShards segments (shard_base); block row r = frame * nbh + bi appends to
+    // segment r % kListShards through its own counter slow_shards[s * kShardStride] (zeroed by
+    // the caller); the list pass adds the segments' lengths into *slow_count.
     uint32_t *slow_list;
     uint32_t *slow_count;
+    uint32_t *slow_shards;
 };
 
 struct EdgeArgs {

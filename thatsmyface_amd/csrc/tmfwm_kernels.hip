@@ -91,12 +91,15 @@ __global__ __launch_bounds__(64, (B > 8 ? 2 : kExtract8Waves)) void extract_kern
     const int lane = threadIdx.x & 63, g = lane / L, q = lane % L;
     float *tile = lds + g * B * LD;
     if constexpr (LIST) {
-        // grid-stride over the list of blocks the strip pass left undecided
-        const uint32_t n = *a.slow_count, per_frame = (uint32_t)a.nbh * (uint32_t)a.nbw;
-        for (uint32_t t0 = blockIdx.x * BPW; t0 < n; t0 += gridDim.x * BPW) {
+        // grid-stride over the list's segments: the blocks the strip pass left undecided
+        const uint32_t per_frame = (uint32_t)a.nbh * (uint32_t)a.nbw, rows = (uint32_t)a.nframes * (uint32_t)a.nbh;
+        for (uint32_t s = blockIdx.x; s < kListShards; s += gridDim.x) {
+          const uint32_t n = a.slow_shards[s * kShardStride], base = shard_base(s, rows, (uint32_t)a.nbw);
+          if (n != 0 && lane == 0) atomicAdd(a.slow_count, n);
+          for (uint32_t t0 = 0; t0 < n; t0 += BPW) {
             StripPos pos;
             pos.valid = t0 + g < n;
-            const uint32_t id = pos.valid ? a.slow_list[t0 + g] : 0u;
+            const uint32_t id = pos.valid ? a.slow_list[base + t0 + g] : 0u;
             pos.frame = id / per_frame;
             const uint32_t rem = id % per_frame;
             pos.bi = (int)(rem / (uint32_t)a.nbw);
@@ -109,6 +112,7 @@ __global__ __launch_bounds__(64, (B > 8 ? 2 : kExtract8Waves)) void extract_kern
                 else a.fb_list[atomicAdd(a.fb_count, 1u)] = id;  // dgesdd route (extract_fixup_kernel)
             }
             __syncthreads();  // the LDS tiles are reused by the next listed blocks
+          }
         }
     } else {
         const StripPos pos = strip_pos<B>(a.strips_per_row, a.nbw);
@@ -118,7 +122,11 @@ __global__ __launch_bounds__(64, (B > 8 ? 2 : kExtract8Waves)) void extract_kern
         if (!pos.valid || q != 0) return;
         const uint32_t id = (uint32_t)(((int64_t)blockIdx.y * a.nbh + pos.bi) * a.nbw + pos.bj);
         if (!ok) {  // the enclosure did not decide f32(sigma_1): list pass, or the dgesdd route
-            if (a.slow_list) a.slow_list[atomicAdd(a.slow_count, 1u)] = id;
+            if (a.slow_list) {
+                const uint32_t row = blockIdx.y * (uint32_t)a.nbh + (uint32_t)pos.bi, s = row % kListShards;
+                a.slow_list[shard_base(s, (uint32_t)a.nframes * (uint32_t)a.nbh, (uint32_t)a.nbw) +
+                            atomicAdd(a.slow_shards + s * kShardStride, 1u)] = id;
+            }
             else a.fb_list[atomicAdd(a.fb_count, 1u)] = id;
             return;
         }
@@ -331,8 +339,8 @@ static hipError_t launch_embed_b(EmbedArgs a, hipStream_t st)
         hipLaunchKernelGGL((embed_kernel<B, false>), dim3((unsigned)gx, (unsigned)nf), dim3(64), 0, st, c);
     }
     if (kDeferMax<B> > 0 && a.slow_list) {  // the list pass over the blocks the first pass left unfinished (ids relative to a.src)
-        const int64_t waves = ((int64_t)a.nframes * a.nbh * a.nbw + Geo<B>::BPW - 1) / Geo<B>::BPW;
-        const unsigned grid = (unsigned)(waves < kListPassGrid ? waves : kListPassGrid);
+        const int64_t rows = a.nframes * a.nbh;  // one wave per segment (2 per SIMD fill the chip)
+        const unsigned grid = (unsigned)(rows < (int64_t)kListShards ? rows : (int64_t)kListShards);
         if constexpr (kDeferMax<B> > 0) hipLaunchKernelGGL((embed_kernel<B, true>), dim3(grid), dim3(64), 0, st, a);
     }
     return hipGetLastError();
@@ -408,8 +416,8 @@ static hipError_t launch_extract_b(ExtractArgs a, hipStream_t st)
         hipLaunchKernelGGL((extract_kernel<B, false>), dim3((unsigned)gx, (unsigned)nf), dim3(64), 0, st, c);
     }
     if (a.slow_list) {  // the list pass over the undecided blocks (ids relative to a.wsrc / a.osrc)
-        const int64_t waves = ((int64_t)a.nframes * a.nbh * a.nbw + Geo<B>::BPW - 1) / Geo<B>::BPW;
-        const unsigned grid = (unsigned)(waves < kListPassGrid ? waves : kListPassGrid);
+        const int64_t rows = a.nframes * a.nbh;  // segments past the rows stay empty
+        const unsigned grid = (unsigned)(rows < (int64_t)kListShards ? rows : (int64_t)kListShards);
         hipLaunchKernelGGL((extract_kernel<B, true>), dim3(grid), dim3(64), 0, st, a);
     }
     return hipGetLastError();
