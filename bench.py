@@ -62,10 +62,11 @@ def parse(argv=None):
     p.add_argument("--lapack-frames", type=int, default=8,
                    help="frames of the parity sample also checked against the reference's own SVD arithmetic "
                         "(the oracle's dgesdd route, ~1 s per 4K frame per 16 cores; 0 = skip)")
-    p.add_argument("--exact-frames", type=int, default=64,
-                   help="hybrid route only: frames of the batch re-run on the GPU's reference route (the dgesdd "
-                        "route for every block, exact by construction) after the timed region, timed and "
-                        "compared byte for byte with the timed run's output (0 = skip)")
+    p.add_argument("--exact-frames", type=int, default=-1,
+                   help="hybrid route only: frames of each rank's batch re-run on the GPU's reference route (the "
+                        "dgesdd route for every block, exact by construction) after the timed region, timed and "
+                        "compared byte for byte with the timed run's output; -1 = every frame (default), 0 = skip; "
+                        "a differing byte fails the run (exit status 3)")
     p.add_argument("--pg-timeout", type=float, default=600.0,
                    help="seconds a rank may wait in a collective before the run fails (N > 1)")
     p.add_argument("--route", default="hybrid", choices=["hybrid", "reference"],
@@ -169,35 +170,48 @@ def gpu_kernels(route="hybrid"):
     )
 
 
-def exact_route_sample(K, frames, tile, out, tiles, block, alpha, n, on_gpu):
-    """The hybrid route's bytes against the reference route's on the first n frames of the
-    timed batch, both on the GPU: the reference route runs the dgesdd route on
-    every block, np.linalg.svd's arithmetic by construction, so this counts the bytes where the
-    throughput route's statistical exactness failed, over far more blocks than the CPU oracle
-    can check.  Also times the reference route (embed + extract of its own output)."""
+def exact_route_check(K, frames, tile, out, tiles, block, alpha, n, on_gpu, chunk=64):
+    """The timed (hybrid-route) output against the reference route's, both on the GPU
+    (DESIGN.md 3.5), over the first n frames of this rank's batch (n < 0: every frame), in
+    chunks of `chunk` frames after the timed region.  The reference route runs the dgesdd route
+    on every block -- np.linalg.svd's arithmetic by construction -- so this compares every timed
+    byte with the reference's arithmetic (watermarking.py:135 embed, :224 extract of the GPU's
+    own watermarked frames).  Also times the reference route (embed + extract per chunk)."""
     import torch
 
-    n = min(n, frames.shape[0])
+    total = frames.shape[0]
+    n = total if n < 0 else min(n, total)
     if n <= 0 or not hasattr(K, "exact_embed"):
         return None
-    f = frames[:n]
-    eo, et = torch.empty_like(f), torch.empty_like(tiles[:n])
-    K.exact_embed(f, tile, block, alpha, eo)  # warm: first call sizes the pools
+    c = min(chunk, n)
+    eo, et = torch.empty_like(frames[:c]), torch.empty_like(tiles[:c])
+    K.exact_embed(frames[:c], tile, block, alpha, eo)  # warm: first call sizes the pools
     sync = torch.cuda.synchronize if on_gpu else (lambda: None)
     sync()
-    t0 = time.perf_counter()
-    K.exact_embed(f, tile, block, alpha, eo)
-    K.exact_extract(eo, f, block, alpha, et)
-    sync()
-    dt = time.perf_counter() - t0
-    H, W = f.shape[1], f.shape[2]
-    diff_e = int((eo != out[:n]).sum())
-    diff_x = int((et != tiles[:n]).sum())
-    return {"frames": n, "blocks": n * (H // block) * (W // block),
+    diff_e = diff_x = frames_e = frames_x = 0
+    dt = 0.0
+    for s in range(0, n, c):
+        e = min(n, s + c)
+        f, m = frames[s:e], e - s
+        t0 = time.perf_counter()
+        K.exact_embed(f, tile, block, alpha, eo[:m])
+        K.exact_extract(eo[:m], f, block, alpha, et[:m])
+        sync()
+        dt += time.perf_counter() - t0
+        de = (eo[:m] != out[s:e]).reshape(m, -1).sum(dim=1)
+        dx = (et[:m] != tiles[s:e]).reshape(m, -1).sum(dim=1)
+        diff_e += int(de.sum())
+        diff_x += int(dx.sum())
+        frames_e += int((de != 0).sum())
+        frames_x += int((dx != 0).sum())
+    H, W = frames.shape[1], frames.shape[2]
+    return {"frames": n, "of_frames": total, "blocks": n * (H // block) * (W // block),
             "embed_bytes_differing": diff_e, "extract_bytes_differing": diff_x,
-            "reference_route_Mpx_per_s": round(n * H * W / dt / 1e6, 1),
-            "what": "the timed (hybrid-route) output vs the GPU reference route (dgesdd route on every block) "
-                    "on the batch's first frames; reference-route rate = embed + extract of those frames"}
+            "frames_differing": max(frames_e, frames_x),
+            "reference_route_Mpx_per_s": round(n * H * W / dt / 1e6, 1) if dt > 0 else None,
+            "what": "every timed (hybrid-route) output byte of these frames vs the GPU reference route (dgesdd "
+                    f"route on every block), {c}-frame chunks after the timed region; reference-route rate = "
+                    "embed + extract of those frames"}
 
 
 def oracle_check(host_frames, host_tile, out, tiles, block, alpha, threads):
@@ -419,9 +433,24 @@ def run(args, kernels=None, device=None):
     achieved = embed_bytes / (embed_ms * 1e-3) / 1e9
     achieved_read = F * embed_read / (embed_ms * 1e-3) / 1e9
 
+    # every rank compares its timed output with the reference route (all of it by default)
     exact = None
-    if rank == 0 and getattr(K, "route", "hybrid") == "hybrid" and args.exact_frames > 0:
-        exact = exact_route_sample(K, frames, wm, rt.out, rt.tiles, b, alpha, args.exact_frames, on_gpu)
+    if getattr(K, "route", "hybrid") == "hybrid" and args.exact_frames != 0:
+        exact = exact_route_check(K, frames, wm, rt.out, rt.tiles, b, alpha, args.exact_frames, on_gpu)
+        if world > 1:
+            cdev = dev if args.backend == "nccl" else "cpu"
+            mine = exact or {}
+            v = torch.tensor([mine.get(k, 0) for k in ("frames", "of_frames", "blocks", "embed_bytes_differing",
+                                                       "extract_bytes_differing", "frames_differing")],
+                             dtype=torch.int64, device=cdev)
+            dist.all_reduce(v)
+            rates = [None] * world
+            dist.all_gather_object(rates, mine.get("reference_route_Mpx_per_s"))
+            if exact is not None:
+                exact = dict(exact, **dict(zip(("frames", "of_frames", "blocks", "embed_bytes_differing",
+                                                "extract_bytes_differing", "frames_differing"), (int(x) for x in v.cpu()))),
+                             reference_route_Mpx_per_s=rates[0], ranks=world,
+                             reference_route_Mpx_per_s_over_ranks=rates)
 
     # parity of the timed batch against the oracle.  N = 1: rank 0 checks the CPU-baseline
     # sample (the batch's first --cpu-frames frames); N > 1: every rank checks its share of
@@ -600,7 +629,7 @@ def run(args, kernels=None, device=None):
             "parity_sample": parity,
             "lapack_route_sample": lapack_sample["summary"] if lapack_sample else None,
             "lapack_route_detail": lapack_sample,
-            "exact_route_sample": exact,
+            "exact_route_check": exact,
             "cpu_baseline": cpu,
             "cpu_baseline_reference_model": structured,
             "lib_build": build,
@@ -616,6 +645,10 @@ def run(args, kernels=None, device=None):
         return 3
     if lapack_sample and (lapack_sample["embed_mismatch"] or lapack_sample["extract_mismatch"]):
         print(f"bench.py: parity vs the dgesdd route FAILED on rank {rank}: {lapack_sample}", file=sys.stderr, flush=True)
+        return 3
+    if exact and (exact["embed_bytes_differing"] or exact["extract_bytes_differing"]):
+        print(f"bench.py: the timed output differs from the GPU reference route on rank {rank}: {exact}",
+              file=sys.stderr, flush=True)
         return 3
     return 0
 

@@ -165,8 +165,8 @@ def test_bench_one_rank_cpu_baselines(tmp_path, capfd):
     line = json.loads([x for x in out.stdout.splitlines() if x.startswith("{")][-1])
     assert line["parity_sample"]["frames"] == 2 and line["parity_sample"]["embed_mismatch"] == 0
     assert line["cpu_baseline"]["kind"] == "port" and line["cpu_baseline"]["value"] > 0
-    ex = line["exact_route_sample"]
-    assert ex["frames"] == 2 and ex["blocks"] == 2 * (H // B) * (W // B)
+    ex = line["exact_route_check"]  # every frame of the batch by default
+    assert ex["frames"] == 2 and ex["of_frames"] == 2 and ex["blocks"] == 2 * (H // B) * (W // B)
     assert ex["embed_bytes_differing"] == 0 and ex["extract_bytes_differing"] == 0 and ex["reference_route_Mpx_per_s"] > 0
     rm = line["cpu_baseline_reference_model"]
     assert rm["value"] > 0 and rm["crops_bit_exact_vs_gpu"].endswith("/2")
