@@ -33,6 +33,8 @@
 #include <omp.h>
 #endif
 
+#include "orc_plan.h"
+
 #define ORC_MAXB 16
 
 /* SVD routes:
@@ -90,22 +92,14 @@ static inline void colour_inv(float y, float cbs, float crs, uint8_t out[3])
     out[2] = u8_from_unit((float)fma(0.0, CR, fma(1.0, Y, 1.773 * CB)));
 }
 
+void orc_colour_inv_px(float y, float cbs, float crs, uint8_t out[3]) { colour_inv(y, cbs, crs, out); }
+
 /* ------------------------------------------------------------------------ */
 /* N3: pocketfft fp32 DCT-II / DCT-III (ortho), every even length 4..16     */
 /* (the UI block sizes, embed_watermark_page.py:324-331).                    */
 /* scipy.fftpack.dct/idct -> pocketfft T_dcst23::exec around rfftp.          */
 /* Every statement below is one fp32 operation (no contraction).             */
 /* ------------------------------------------------------------------------ */
-typedef struct {
-    int n;
-    int nf;
-    int fct[4];            /* rfftp factor list (pocketfft factorize: 4s, then a 2 moved to the front, then odd) */
-    float tw[4][3 * 16];   /* rfftp twiddles per factor: tw[k][(j-1)*(ido-1) + 2i-2 / 2i-1] */
-    float tws[4][2 * 16];  /* generic-radix (ip > 5) table: tws[2m], tws[2m+1] = cos, sin(2 pi m / ip) */
-    float dtw[16];         /* DCT twiddle[i] = cos(2 pi (i+1) / (4n)) */
-    float norm;            /* f32(1/sqrt(2n)) (scipy norm_fct, ortho) */
-} dct_plan;
-
 #define ORC_NPLANS 7 /* n = 4, 6, ..., 16 */
 static dct_plan g_plans[ORC_NPLANS];
 static int g_plans_ready = 0;
@@ -211,6 +205,8 @@ static const dct_plan *plan_for(int n)
     plans_init();
     return &g_plans[(n - 4) / 2];
 }
+
+const dct_plan *orc_plan(int n) { return plan_for(n); }
 
 #define PM(a, b, c, d) do { float c_ = (c), d_ = (d); (a) = c_ + d_; (b) = c_ - d_; } while (0)
 #define MULPM(a, b, c, d, e, f) do { float c_ = (c), d_ = (d), e_ = (e), f_ = (f); (a) = c_ * e_ + d_ * f_; (b) = c_ * f_ - d_ * e_; } while (0)
@@ -1114,8 +1110,11 @@ int orc_svd_flag(const double *sig, int b)
     return m * ORC_FLAG_T < s1;
 }
 
-/* One block's factors by route; returns 1 when the dgesdd route produced them. */
-int orc_svd_block_mode(const float *D, int b, int mode, float *U, float *S, float *Vt)
+/* One block's factors by route; returns 1 when the dgesdd route produced them.  The hybrid
+ * route also needs the block's watermark byte, alpha and chroma for its byte certificate
+ * (tmfwm_cert.cpp); cbs == NULL skips the certificate (the conditioning test alone). */
+static int svd_block_route(const float *D, int b, int mode, float *U, float *S, float *Vt, uint8_t w, double alpha,
+                           const float *cbs, const float *crs)
 {
     if (mode == ORC_SVD_LAPACK) {
         orc_lp_svd_block_f32(D, b, U, S, Vt);
@@ -1123,7 +1122,8 @@ int orc_svd_block_mode(const float *D, int b, int mode, float *U, float *S, floa
     }
     double U64[ORC_MAXB * ORC_MAXB], V64[ORC_MAXB * ORC_MAXB], sig[ORC_MAXB];
     orc_svd_block_f64(D, b, U64, sig, V64);
-    if (mode == ORC_SVD_HYBRID && orc_svd_flag(sig, b)) {
+    if (mode == ORC_SVD_HYBRID &&
+        (orc_svd_flag(sig, b) || (cbs && orc_cert_block(U64, sig, V64, b, w, alpha, cbs, crs, NULL)))) {
         orc_lp_svd_block_f32(D, b, U, S, Vt);
         return 1;
     }
@@ -1132,6 +1132,11 @@ int orc_svd_block_mode(const float *D, int b, int mode, float *U, float *S, floa
         for (int r = 0; r < b; ++r) { U[r * b + k] = (float)U64[r * b + k]; Vt[k * b + r] = (float)V64[r * b + k]; }
     }
     return 0;
+}
+
+int orc_svd_block_mode(const float *D, int b, int mode, float *U, float *S, float *Vt)
+{
+    return svd_block_route(D, b, mode, U, S, Vt, 0, 0.0, NULL, NULL);
 }
 
 /* sigma_1 by route: the Jacobi value, or LAPACK's S[0] (the reference's value; the
@@ -1305,19 +1310,27 @@ void orc_scatter_blocks(const float *blocks, int H, int W, int b, float *Y)
         }
 }
 
-/* One block row (bi) of the embed: Y plane updated in place. */
-static int64_t embed_block_row(float *Y, int W, int b, int bi, int nbw, const uint8_t *wm, double alpha, int mode)
+/* One block row (bi) of the embed: Y plane updated in place (ycc: the frame's Cb, Cr). */
+static int64_t embed_block_row(float *Y, const float *ycc, int W, int b, int bi, int nbw, const uint8_t *wm, double alpha,
+                               int mode)
 {
     int64_t fallback = 0;
     const dct_plan *p = plan_for(b);
     float D[ORC_MAXB * ORC_MAXB], U[ORC_MAXB * ORC_MAXB], Vt[ORC_MAXB * ORC_MAXB], S[ORC_MAXB], M[ORC_MAXB * ORC_MAXB];
+    float cbs[ORC_MAXB * ORC_MAXB], crs[ORC_MAXB * ORC_MAXB];
     for (int bj = 0; bj < nbw; ++bj) {
         for (int r = 0; r < b; ++r)
-            for (int c = 0; c < b; ++c) D[r * b + c] = Y[(int64_t)(bi * b + r) * W + bj * b + c];
-        dct2d(p, D, 0);                                    /* :192 */
-        fallback += orc_svd_block_mode(D, b, mode, U, S, Vt); /* :195 */
-        orc_blend_reconstruct(U, S, Vt, b, wm[(int64_t)bi * nbw + bj], alpha, M); /* :198-201 */
-        dct2d(p, M, 1);                                    /* :204 */
+            for (int c = 0; c < b; ++c) {
+                const int64_t q = (int64_t)(bi * b + r) * W + bj * b + c;
+                D[r * b + c] = Y[q];
+                cbs[r * b + c] = ycc[3 * q + 1];
+                crs[r * b + c] = ycc[3 * q + 2];
+            }
+        const uint8_t w = wm[(int64_t)bi * nbw + bj];
+        dct2d(p, D, 0);                                                     /* :192 */
+        fallback += svd_block_route(D, b, mode, U, S, Vt, w, alpha, cbs, crs); /* :195 */
+        orc_blend_reconstruct(U, S, Vt, b, w, alpha, M);                   /* :198-201 */
+        dct2d(p, M, 1);                                                     /* :204 */
         for (int r = 0; r < b; ++r)
             for (int c = 0; c < b; ++c) Y[(int64_t)(bi * b + r) * W + bj * b + c] = M[r * b + c]; /* :207-210 */
     }
@@ -1347,7 +1360,7 @@ int orc_embed_frame_mode(const uint8_t *rgb, int H, int W, const uint8_t *wm, in
     const int nbh = H / b, nbw = W / b;
     int64_t fallback = 0;
 #pragma omp parallel for num_threads(nthreads) schedule(dynamic, 1) reduction(+ : fallback)
-    for (int bi = 0; bi < nbh; ++bi) fallback += embed_block_row(Y, W, b, bi, nbw, wm, alpha, mode);
+    for (int bi = 0; bi < nbh; ++bi) fallback += embed_block_row(Y, ycc, W, b, bi, nbw, wm, alpha, mode);
 #pragma omp parallel for num_threads(nthreads) schedule(static)
     for (int64_t q = 0; q < npix; ++q) colour_inv(Y[q], ycc[3 * q + 1], ycc[3 * q + 2], out + 3 * q);
     free(ycc);
