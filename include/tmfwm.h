@@ -26,7 +26,9 @@
  * slider values (others return TMFWM_ERR_UNSUPPORTED).
  *
  * SVD routes: every block goes through a fused Jacobi SVD; the
- * blocks whose factors could round differently from LAPACK's (conditioning test) are
+ * blocks whose factors could round differently from LAPACK's (conditioning test) and,
+ * since ABI 9, every block whose output bytes the byte certificate cannot prove equal to
+ * LAPACK's (interval arithmetic through the reconstruct, IDCT and inverse colour) are
  * redone by a second pass on the dgesdd route -- numpy's np.linalg.svd restated
  * operation by operation (LAPACK 3.12 + OpenBLAS 0.3.29 SkylakeX kernels) -- so the
  * bytes are the reference's.  The _ex entry points report how many blocks took it.
@@ -40,14 +42,15 @@
 extern "C" {
 #endif
 
-#define TMFWM_ABI_VERSION 8
+#define TMFWM_ABI_VERSION 9
 
 #define TMFWM_MEM_HOST 0
 #define TMFWM_MEM_DEVICE 1
 
 /* SVD routes of embed / extract (tmfwm_embed_route, tmfwm_extract_route) */
 #define TMFWM_ROUTE_HYBRID 0    /* Jacobi on every block, the dgesdd route for the blocks the
-                                   conditioning test flags (the throughput route: tmfwm_embed) */
+                                   conditioning test flags or whose bytes the certificate cannot
+                                   prove (the throughput route: tmfwm_embed) */
 #define TMFWM_ROUTE_REFERENCE 1 /* the dgesdd route -- np.linalg.svd's own arithmetic -- for every
                                    block: the reference's bytes by construction */
 
@@ -196,6 +199,10 @@ int tmfwm_embed_multi_route(const uint8_t *rgb, int64_t n_frames, int32_t height
 int tmfwm_extract_multi_route(const uint8_t *wm_rgb, const uint8_t *orig_rgb, int64_t n_frames, int32_t height, int32_t width,
                               int64_t frame_stride, int32_t block, double alpha, uint8_t *out_tiles, const int32_t *devices,
                               int32_t n_shards, int32_t route, int64_t *n_lapack_blocks);
+
+/* Frees the device staging buffers the multi-GPU calls keep between calls (at most four free
+ * buffers per device are kept; ABI 9).  Returns the number of buffers freed. */
+int tmfwm_release_cached_buffers(void);
 
 /* rgb_to_ycbcr (watermarking.py:23): npix RGB uint8 pixels -> npix x 3 float32 (Y, Cb+0.5, Cr+0.5). */
 int tmfwm_rgb_to_ycbcr(const uint8_t *rgb, int64_t npix, float *ycc, int32_t mem_kind, void *hip_stream);

@@ -108,10 +108,13 @@ def test_bench_eight_ranks_gloo(tmp_path):
     assert line["n_ranks"] == 8 and line["config"]["frames_total"] == 8 * F
     assert line["parity_sample"]["frames"] == 16 and line["parity_sample"]["embed_mismatch"] == 0
     assert line["lapack_route_sample"] == "8/8"
-    # self-contained N > 1 line: rank 0's CPU baseline on cores / N and the
-    # spread of the ranks' mean launch times
+    # self-contained N > 1 line: the host's CPU baseline -- every rank's share
+    # checked concurrently, all ranks' pixels over the slowest rank's time -- and the spread of the
+    # ranks' mean launch times; every frame of every shard checked against the reference route
     cb = line["cpu_baseline"]
-    assert cb and cb["kind"] == "port" and cb["value"] > 0 and cb["cores"] >= 1 and "rank 0's share" in cb["sample"]
+    assert cb and cb["kind"] == "port" and cb["value"] > 0 and cb["cores"] >= 8 and len(cb["per_rank_s"]) == 8
+    ex = line["exact_route_check"]
+    assert ex["ranks"] == 8 and ex["frames"] == ex["of_frames"] == 8 * F and ex["embed_bytes_differing"] == 0
     lm = line["roofline"]["launch_ms_over_ranks"]
     assert lm["ranks"] == 8 and 0 < lm["min"] <= line["roofline"]["launch_ms"] <= lm["max"]
     xm = line["kernels_ms"]["extract_over_ranks"]

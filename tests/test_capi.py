@@ -38,7 +38,7 @@ def test_nm_exports_match_header():
 
 def test_abi_version_and_device_count():
     L = _lib.load()
-    assert L.tmfwm_abi_version() == _lib.ABI_VERSION == 8
+    assert L.tmfwm_abi_version() == _lib.ABI_VERSION == 9
     assert _lib.device_count() >= 0
 
 

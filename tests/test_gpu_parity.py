@@ -793,6 +793,10 @@ def test_multi_entry_points_logical_shards(dev, monkeypatch):
             assert np.array_equal(out[f], ref), (shards, f)
             assert np.array_equal(ext[f], O.extract_frame(ref, host[f], b, 0.1)), (shards, f)
     assert torch.cuda.current_device() == 0
+    # the staging buffers kept between calls (at most four per device) can be freed, and the next
+    # call allocates afresh
+    assert 0 < multi.release_cached_buffers() <= 4 and multi.release_cached_buffers() == 0
+    assert np.array_equal(multi.embed_multi(host, t, b, 0.1, devices=[0, 0]), ref_dev)
 
 
 def test_payload_round_trip_dropin_gpu(dev):
@@ -852,12 +856,14 @@ def test_reference_route_full_4k_vs_oracle_lapack(dev, b):
 
 
 @pytest.mark.parametrize("b", [8, 16])
-def test_hybrid_vs_reference_route_4k(dev, b):
-    """The hybrid route's bytes against the reference route's on 32 camera-like 4K frames
-    (tools/exp/route_diff_gpu.py at test size): at b = 8 none differ (0 over
-    99.5 M blocks in profiles/r04/r04f/); at b = 16 the measured rate is ~1 byte per 8 M
-    blocks, so at most a few of these 1.04 M blocks may differ, each by one embed byte.
-    Extract of the same watermarked frames agrees on both routes (its enclosure is a proof)."""
+@pytest.mark.parametrize("wm", ["noise", "qr"])
+def test_hybrid_vs_reference_route_4k(dev, b, wm):
+    """The hybrid route's bytes equal the reference route's (np.linalg.svd's arithmetic on every
+    block) on 32 camera-like 4K frames: the byte certificate sends every block
+    whose bytes it cannot prove to the dgesdd route.  Round 4, without it, measured 5 differing
+    bytes over 91.3 M blocks at b = 16.  A binary (QR-code) watermark leaves half the blocks at
+    w = 0, where the bytes sit on truncation boundaries.  Extract of the same
+    watermarked frames agrees on both routes (its enclosure is a proof)."""
     import sys as _sys
 
     _sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "exp"))
@@ -867,17 +873,17 @@ def test_hybrid_vs_reference_route_4k(dev, b):
 
     H, W, n = 2160, 3840, 32
     fr = photo_covers(n, H, W, 77 + b, dev)
-    tile = batch.synth_tile(H // b, W // b, device=dev)
+    if wm == "qr":
+        tile = torch.from_numpy(_u8(78 + b, (H // b, W // b)) & np.uint8(1)).to(dev) * 255
+    else:
+        tile = batch.synth_tile(H // b, W // b, device=dev)
     oh = batch.embed_batch(fr, tile, b, 0.1, route="hybrid")
     orf = batch.embed_batch(fr, tile, b, 0.1, route="reference")
     xs = batch.extract_batch(orf, fr, b, 0.1, route="hybrid")
     xr = batch.extract_batch(orf, fr, b, 0.1, route="reference")
     nb = blocks_differing(oh, orf, b)
     assert torch.equal(xs, xr)
-    if b == 8:
-        assert nb == 0 and torch.equal(oh, orf)
-    else:
-        assert nb <= 4 and int((oh != orf).sum()) <= 4 * 3, nb
+    assert nb == 0 and torch.equal(oh, orf), nb
 
 
 @pytest.mark.parametrize("mem", ["host", "device"])
@@ -981,6 +987,12 @@ def test_dropin_zero_copy_pil_path(dev, monkeypatch):
     gc.collect()
     c = W.embed_watermark(cover, wm, False, cfg)
     assert c._tmfwm_rgbx.ctypes.data == buf and np.array_equal(np.asarray(c), np.asarray(a))
+    # a Pillow without the Arrow interface (< 11.2): the copying path, same images
+    monkeypatch.setattr(W, "_pa", None)
+    monkeypatch.delattr(Image, "fromarrow", raising=False)
+    d = W.embed_watermark(cover, wm, False, cfg)
+    assert not hasattr(d, "_tmfwm_rgbx") and np.array_equal(np.asarray(d), np.asarray(a))
+    assert np.array_equal(np.asarray(W.extract_watermark(d, cover, cfg)), np.asarray(W.extract_watermark(a, cover, cfg)))
 
 
 def test_multi_entry_points_reference_route(dev):

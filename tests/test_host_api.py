@@ -100,3 +100,13 @@ def test_zero_copy_pil_helpers():
     del out, buf  # the pool counts every reference, this test's own included
     gc.collect()
     assert W._take_out(48 * 80 * 4).ctypes.data == where
+
+
+def test_zero_copy_needs_pillow_arrow(monkeypatch):
+    """Pillow < 11.2 has no Image.fromarrow / __arrow_c_array__ (the reference allows Pillow >= 9,
+    requirements.txt:3): the drop-in must then take the copying path, pyarrow or not."""
+    monkeypatch.setattr(W, "_pa", None)
+    monkeypatch.setattr(W, "_zero_copy", True)
+    monkeypatch.delattr(Image, "fromarrow", raising=False)
+    assert W._arrow() is None and W._zero_copy is False
+    assert W._rgbx_view(Image.new("RGB", (8, 8))) is None

@@ -14,7 +14,7 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # TMFWM_LIB selects an alternative build (e.g. the phase-profile libtmfwm_stamps.so)
 LIB_PATH = os.environ.get("TMFWM_LIB") or os.path.join(_HERE, "libtmfwm.so")
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 MEM_HOST = 0
 MEM_DEVICE = 1
@@ -72,6 +72,7 @@ SIGNATURES = {
     "tmfwm_embed_px": (ctypes.c_int, [_VP, _I32, _I64, _I64, _I32, _I32, _VP, _I32, _D, _VP, _I32, _I64, _I32, _VP, _I32, _VP]),
     "tmfwm_extract_px": (ctypes.c_int, [_VP, _I32, _I64, _VP, _I32, _I64, _I64, _I32, _I32, _I32, _D, _VP, _I32, _VP, _I32, _VP]),
     "tmfwm_embed_multi": (ctypes.c_int, [_VP, _I64, _I32, _I32, _I64, _VP, _I32, _D, _VP, _VP, _I32, _VP]),
+    "tmfwm_release_cached_buffers": (ctypes.c_int, []),
     "tmfwm_extract_multi": (ctypes.c_int, [_VP, _VP, _I64, _I32, _I32, _I64, _I32, _D, _VP, _VP, _I32, _VP]),
     "tmfwm_embed_multi_route": (ctypes.c_int, [_VP, _I64, _I32, _I32, _I64, _VP, _I32, _D, _VP, _VP, _I32, _I32, _VP]),
     "tmfwm_extract_multi_route": (ctypes.c_int, [_VP, _VP, _I64, _I32, _I32, _I64, _I32, _D, _VP, _VP, _I32, _I32, _VP]),

@@ -125,6 +125,51 @@ TMF_DEVI void dct2d_rows_layout(float (&x)[Geo<B>::R][B], float *tile, int q)
     __syncthreads();
 }
 
+// The same 2-D IDCT on intervals: lower ends through `tl`, upper ends through
+// `th` (both [B][B+1] tiles of this block), every pass on Ivf end points.
+template <int B>
+TMF_DEVI void idct2d_rows_layout_iv(float (&xl)[Geo<B>::R][B], float (&xh)[Geo<B>::R][B], float *tl, float *th, int q)
+{
+    constexpr int R = Geo<B>::R, LD = B + 1;
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+        if (real_row<B>(q, r))
+#pragma unroll
+            for (int c = 0; c < B; ++c) {
+                tl[(q * R + r) * LD + c] = xl[r][c];
+                th[(q * R + r) * LD + c] = xh[r][c];
+            }
+    __syncthreads();
+#pragma unroll
+    for (int cc = 0; cc < R; ++cc) {
+        if (!real_row<B>(q, cc)) continue;
+        Ivf col[B];
+#pragma unroll
+        for (int r = 0; r < B; ++r) col[r] = {tl[r * LD + q * R + cc], th[r * LD + q * R + cc]};
+        dct::dct3<B>(col);
+#pragma unroll
+        for (int r = 0; r < B; ++r) {
+            tl[r * LD + q * R + cc] = col[r].lo;
+            th[r * LD + q * R + cc] = col[r].hi;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        Ivf row[B];
+#pragma unroll
+        for (int c = 0; c < B; ++c)
+            row[c] = real_row<B>(q, r) ? Ivf{tl[(q * R + r) * LD + c], th[(q * R + r) * LD + c]} : Ivf{0.0f, 0.0f};
+        dct::dct3<B>(row);
+#pragma unroll
+        for (int c = 0; c < B; ++c) {
+            xl[r][c] = real_row<B>(q, r) ? row[c].lo : 0.0f;
+            xh[r][c] = real_row<B>(q, r) ? row[c].hi : 0.0f;
+        }
+    }
+    __syncthreads();
+}
+
 struct StripPos {
     int64_t frame;
     int bi, bj;
@@ -183,7 +228,7 @@ TMF_DEVI void luma_rows(const uint32_t (&words)[Geo<B>::R][Geo<B>::NW], float (&
 // one wave per SIMD).  Forcing 2 for b = 12 / 16 costs 156 / 256 B of scratch per lane
 // and is faster: embed<12> 283 -> 201 us, embed<16> 531 -> 345 us per 4K frame.
 template <int B>
-constexpr int kEmbedWaves = (B == 12 || B == 16) ? 2 : 1;
+constexpr int kEmbedWaves = (B == 8 || B == 12 || B == 14 || B == 16) ? 2 : 1;
 
 // Strip pass: once at most kDeferMax blocks of a wave still need f64 sweeps after a sweep
 // and its Newton try, the wave leaves them to the list pass instead of running another
@@ -207,15 +252,33 @@ constexpr int kEmbedTS0 = B * (B + 1) > kScratchFloats<B, Geo<B>::L> ? B * (B + 
 template <int B>
 constexpr int kEmbedTS = ((kParkD<B> && kParkOff<Geo<B>::L> + B * B > kEmbedTS0<B> ? kParkOff<Geo<B>::L> + B * B : kEmbedTS0<B>) + 1) & ~1;
 
+// Byte certificate of the hybrid route (oracle tmfwm_cert.cpp): LAPACK's f64
+// factors lie within E_k = kCertScale s1 / g_k of the Jacobi route's, every singular value
+// within kCertScale s1 (K = 256 units of 2^-53 s1 / g_k; LAPACK's own V is off by up to 94,
+// the Jacobi route's by up to 30, tools/exp/cert_study.py).
+constexpr double kCertScale = 0x1p-45;
+
+// LDS of one wave: `lds` holds each block's [B][B+1] transpose tile (or svd3's scratch if
+// larger); `lds2` first parks this lane's source bytes during the SVD, then holds the
+// certificate's upper-end tiles ([B][B+1] floats per block)
+template <int B>
+constexpr int kPixWords = Geo<B>::R * Geo<B>::NW * 64;
+template <int B>
+constexpr int kHiTile = B * (B + 1);
+template <int B>
+constexpr int kLds2Floats = kPixWords<B> > Geo<B>::BPW * kHiTile<B> ? kPixWords<B> : Geo<B>::BPW * kHiTile<B>;
+
 // One wave's blocks: strip mode (LIST = false: the strip of blockIdx) or list mode (pos and
 // id from the slow list).  id = (frame * nbh + bi) * nbw + bj, relative to a.src.
 template <int B, bool LIST>
-TMF_DEVI void embed_blocks(const EmbedArgs &a, const StripPos &pos, uint32_t id, float *lds, uint32_t (*pix)[64])
+TMF_DEVI void embed_blocks(const EmbedArgs &a, const StripPos &pos, uint32_t id, float *lds, float *lds2)
 {
     constexpr int L = Geo<B>::L, R = Geo<B>::R, LD = B + 1, NW = Geo<B>::NW, TS = kEmbedTS<B>;
     constexpr bool kPark = kParkD<B>;
     const int lane = threadIdx.x & 63, g = lane / L, q = lane % L;
     float *tile = lds + g * TS;
+    float *tile2 = lds2 + g * kHiTile<B>;
+    uint32_t (*pix)[64] = reinterpret_cast<uint32_t (*)[64]>(lds2);
     const uint8_t *src = a.src + pos.frame * a.frame_stride;
     uint8_t *dst = a.dst + pos.frame * a.frame_stride;
 
@@ -243,56 +306,54 @@ TMF_DEVI void embed_blocks(const EmbedArgs &a, const StripPos &pos, uint32_t id,
         a.slow_list[shard_base(s, (uint32_t)a.nframes * (uint32_t)a.nbh, (uint32_t)a.nbw) +
                     atomicAdd(a.slow_shards + s * kShardStride, 1u)] = id;
     }
+    // this lane's source bytes back to registers: their LDS becomes the upper-end tiles
+    uint32_t words[R][NW];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int i = 0; i < NW; ++i) words[r][i] = pix[r * NW + i][lane];
+    __syncthreads();
 
-    // singular values, U = A / sigma, sort descending (oracle orc_svd_block)
+    // singular values (oracle orc_svd_block: sigma_k = |a_k|, u_k = a_k / sigma_k)
     double sig[B];
-    float U[R][B], Vf[R][B];
 #pragma unroll
     for (int k = 0; k < B; ++k) sig[k] = cdot_part<R, B>(A, k, k);
 #pragma unroll
+    for (int k = 0; k < B; ++k) sig[k] = __builtin_sqrt(group_sum<L>(sig[k]));
+    // Conditioning test (oracle orc_svd_flag): m = min over triplets reaching the
+    // output (f32(sigma_k) != 0) of g_k = min(sigma_k, distance to the nearest other sigma); the
+    // block takes the dgesdd route iff m * 2^20 < sigma_1.  (Per-k minima first: folding every
+    // pair into one running minimum is the same value but a 36-deep dependent chain, +1.5 % on
+    // embed<8>, profiles/r03/r03r.)
+    double gk[B], s1 = 0.0;
+#pragma unroll
     for (int k = 0; k < B; ++k) {
-        sig[k] = __builtin_sqrt(group_sum<L>(sig[k]));
-        const double inv = 1.0 / sig[k];
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            U[r][k] = sig[k] == 0.0 ? 0.0f : (float)(A[r][k] * inv);
-            Vf[r][k] = (float)V[r][k];
-        }
+        gk[k] = sig[k];
+        s1 = sig[k] > s1 ? sig[k] : s1;
     }
-    // Conditioning test (oracle orc_svd_flag): a block whose factors could
-    // round differently from LAPACK's goes to the dgesdd route (embed_fixup_kernel).
-    // m = min over triplets reaching the output (f32(sigma_k) != 0) of min(sigma_k,
-    // distance to the nearest other sigma); flagged iff m * 2^20 < sigma_1.  (Per-k minima
-    // first: folding every pair into one running minimum is the same value but a 36-deep
-    // dependent chain, +1.5 % on embed<8>, profiles/r03/r03r.)
-    {
-        double g[B], s1 = 0.0;
 #pragma unroll
-        for (int k = 0; k < B; ++k) {
-            g[k] = sig[k];
-            s1 = sig[k] > s1 ? sig[k] : s1;
+    for (int k = 0; k < B; ++k)
+#pragma unroll
+        for (int j = k + 1; j < B; ++j) {
+            const double d = __builtin_fabs(sig[k] - sig[j]);
+            gk[k] = d < gk[k] ? d : gk[k];
+            gk[j] = d < gk[j] ? d : gk[j];
         }
+    double m = s1;
 #pragma unroll
-        for (int k = 0; k < B; ++k)
+    for (int k = 0; k < B; ++k) m = ((float)sig[k] != 0.0f && gk[k] < m) ? gk[k] : m;
+    const bool zero = s1 == 0.0;  // N6: D == 0 -> U = I, Vt = I on both routes
+    const bool flag20 = m * 1048576.0 < s1;
+    // Byte certificate: the interval bounds of the blocks whose bytes it decides (zero,
+    // flagged and deferred blocks keep point intervals: the point path's values)
+    const bool cert = !zero && !flag20 && !slow;
+    const double tE = cert ? kCertScale * s1 : 0.0;
+    double E[B];
+    bool keep[B];
 #pragma unroll
-            for (int j = k + 1; j < B; ++j) {
-                const double d = __builtin_fabs(sig[k] - sig[j]);
-                g[k] = d < g[k] ? d : g[k];
-                g[j] = d < g[j] ? d : g[j];
-            }
-        double m = s1;
-#pragma unroll
-        for (int k = 0; k < B; ++k) m = ((float)sig[k] != 0.0f && g[k] < m) ? g[k] : m;
-        if (m * 1048576.0 < s1 && pos.valid && !slow && q == 0) a.fb_list[atomicAdd(a.fb_count, 1u)] = id;
-    }
-    bool zero = true;
-#pragma unroll
-    for (int k = 0; k < B; ++k) zero = zero && (sig[k] == 0.0);
-    if (zero) {  // N6: D == 0 -> U = I, Vt = I
-#pragma unroll
-        for (int r = 0; r < R; ++r)
-#pragma unroll
-            for (int k = 0; k < B; ++k) U[r][k] = Vf[r][k] = (q * R + r == k) ? 1.0f : 0.0f;
+    for (int k = 0; k < B; ++k) {
+        keep[k] = zero || (float)sig[k] != 0.0f;
+        E[k] = cert && keep[k] ? tE / gk[k] : 0.0;
     }
     // Sort descending (oracle: odd-even transposition sort, stable) as ranks: k goes to
     // position rk[k] = #{j < k: sig[j] >= sig[k]} + #{j > k: sig[j] > sig[k]}.  The
@@ -308,65 +369,134 @@ TMF_DEVI void embed_blocks(const EmbedArgs &a, const StripPos &pos, uint32_t id,
             rk[k] += ge;
             rk[j] += 1 - ge;
         }
-    double top = sig[0];
-#pragma unroll
-    for (int k = 1; k < B; ++k) top = sig[k] > top ? sig[k] : top;
-
-    // N7 blend (:198): S[0] = f32(f64(S[0]) + alpha * (w / 255.0)), S[0] the largest
+    // N7 blend (:198): S[0] = f32(f64(S[0]) + alpha * (w / 255.0)), S[0] the largest; as
+    // intervals [f32(max(sigma - Es, 0)), f32(sigma + Es)] blended at both ends
     const uint32_t wv = pos.valid ? a.wm[(int64_t)pos.bi * a.nbw + pos.bj] : 0u;
-    const float s0 = (float)((double)(float)top + a.alpha * ((double)wv / 255.0));
-    float Us[R][B];
-#pragma unroll
-    for (int r = 0; r < R; ++r)
-        if (real_row<B>(q, r))
-#pragma unroll
-            for (int k = 0; k < B; ++k) tile[(q * R + r) * LD + rk[k]] = U[r][k];
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < R; ++r)
-#pragma unroll
-        for (int t = 0; t < B; ++t) Us[r][t] = real_row<B>(q, r) ? tile[(q * R + r) * LD + t] : 0.0f;
-    __syncthreads();
-
-    // N8 (:201): Bm[t][j] = S'[t] * Vt[t][j] (this lane's rows j of V, row t = rank), then M = U @ Bm
+    const double cw = a.alpha * ((double)wv / 255.0);
+    float Sl[B], Sh[B];
+    bool neg = false;  // alpha < 0 pushing S'[0] below zero: outside the certificate's S' >= 0
 #pragma unroll
     for (int k = 0; k < B; ++k) {
-        const float sk = rk[k] == 0 ? s0 : (float)sig[k];
+        const double lo = sig[k] - tE;
+        Sl[k] = (float)(lo > 0.0 ? lo : 0.0);
+        Sh[k] = (float)(sig[k] + tE);
+        if (rk[k] == 0) {
+            Sl[k] = (float)((double)Sl[k] + cw);
+            Sh[k] = (float)((double)Sh[k] + cw);
+            neg = !(Sl[k] >= 0.0f);
+        }
+    }
+    // U = A / sigma as f32 intervals [f32(u - E), f32(u + E)]; triplets that do not reach the
+    // output (f32(sigma) == 0) take U = [2, 2] against B = [-2 S', 2 S'] (|f32 entries| <= 1)
+    bool straddle = false;  // an interval of a triplet that reaches the output contains 0
 #pragma unroll
-        for (int r = 0; r < R; ++r)
-            if (real_row<B>(q, r)) tile[rk[k] * LD + q * R + r] = sk * Vf[r][k];
+    for (int k = 0; k < B; ++k) {
+        const double inv = 1.0 / sig[k];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            float ul, uh;
+            if (zero) {
+                ul = uh = (q * R + r == k) ? 1.0f : 0.0f;
+            } else if (!keep[k]) {
+                ul = uh = 2.0f;
+            } else {
+                const double u = A[r][k] * inv;
+                ul = (float)(u - E[k]);
+                uh = (float)(u + E[k]);
+                straddle = straddle || (ul < 0.0f && uh > 0.0f);
+            }
+            if (real_row<B>(q, r)) {
+                tile[(q * R + r) * LD + rk[k]] = ul;
+                tile2[(q * R + r) * LD + rk[k]] = uh;
+            }
+        }
+    }
+    __syncthreads();
+    float Ul[R][B], Uh[R][B];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int t = 0; t < B; ++t) {
+            Ul[r][t] = real_row<B>(q, r) ? tile[(q * R + r) * LD + t] : 0.0f;
+            Uh[r][t] = real_row<B>(q, r) ? tile2[(q * R + r) * LD + t] : 0.0f;
+        }
+    __syncthreads();
+
+    // N8 (:201): Bm[t][j] = S'[t] * Vt[t][j] (this lane's rows j of V, row t = rank), then M = U @ Bm,
+    // both ends (S' >= 0: the lower end is S'lo v if v >= 0, else S'hi v; the upper alike)
+#pragma unroll
+    for (int k = 0; k < B; ++k) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            float bl, bh;
+            if (zero) {
+                bl = bh = Sl[k] * ((q * R + r == k) ? 1.0f : 0.0f);
+            } else if (!keep[k]) {
+                bl = -2.0f * Sh[k];
+                bh = 2.0f * Sh[k];
+            } else {
+                const float vl = (float)(V[r][k] - E[k]), vh = (float)(V[r][k] + E[k]);
+                straddle = straddle || (vl < 0.0f && vh > 0.0f);
+                bl = vl >= 0.0f ? Sl[k] * vl : Sh[k] * vl;
+                bh = vh <= 0.0f ? Sl[k] * vh : Sh[k] * vh;
+            }
+            if (real_row<B>(q, r)) {
+                tile[rk[k] * LD + q * R + r] = bl;
+                tile2[rk[k] * LD + q * R + r] = bh;
+            }
+        }
     }
     __syncthreads();
     // k outermost: each element of Bm is read from LDS once and used by this lane's R rows at
-    // once.  Row by row, the compiler hoisted all b^2 reads across the rows and spilled them:
-    // 40 of embed<16>'s 47 spilled VGPRs (scratch traffic ~1x the frame's bytes); this order
-    // keeps 7 (A/B on one box, identical hashes: embed<16> -0.9 % noise / -1.7 % camera-like
-    // covers, embed<8> / <12> +-0, profiles/r04/r04b/ab_*.log).  Every M[r][j] is the same fma
-    // chain over k = 0..b-1.
+    // once (row by row, the compiler hoisted all b^2 reads across the rows and spilled them,
+    // profiles/r04/r04b).  Every M[r][j] is the fma chain over k = 0..b-1; on intervals, the
+    // lower end takes the corner of the smallest product: u's lower end if b >= 0, else its
+    // upper one, and b's lower end if u >= 0, else its upper one (exact when neither interval
+    // contains 0, or one of them is a point; otherwise the wave takes all four corners).
+    float Ml[R][B], Mh[R][B];
 #pragma unroll
     for (int r = 0; r < R; ++r)
 #pragma unroll
-        for (int j = 0; j < B; ++j) x[r][j] = 0.0f;
+        for (int j = 0; j < B; ++j) Ml[r][j] = Mh[r][j] = 0.0f;
+    if (__builtin_amdgcn_ballot_w64(straddle && cert) == 0) {
 #pragma unroll
-    for (int k = 0; k < B; ++k)
+        for (int k = 0; k < B; ++k)
 #pragma unroll
-        for (int j = 0; j < B; ++j) {
-            const float bkj = tile[k * LD + j];
+            for (int j = 0; j < B; ++j) {
+                const float bl = tile[k * LD + j], bh = tile2[k * LD + j];
+                const bool bp = bl >= 0.0f;
 #pragma unroll
-            for (int r = 0; r < R; ++r) x[r][j] = __builtin_fmaf(Us[r][k], bkj, x[r][j]);
-        }
+                for (int r = 0; r < R; ++r) {
+                    const bool up = Ul[r][k] >= 0.0f;
+                    Ml[r][j] = __builtin_fmaf(bp ? Ul[r][k] : Uh[r][k], up ? bl : bh, Ml[r][j]);
+                    Mh[r][j] = __builtin_fmaf(bp ? Uh[r][k] : Ul[r][k], up ? bh : bl, Mh[r][j]);
+                }
+            }
+    } else {
+#pragma unroll
+        for (int k = 0; k < B; ++k)
+#pragma unroll
+            for (int j = 0; j < B; ++j) {
+                const float bl = tile[k * LD + j], bh = tile2[k * LD + j];
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const float ul = Ul[r][k], uh = Uh[r][k], lo = Ml[r][j], hi = Mh[r][j];
+                    Ml[r][j] = __builtin_fminf(__builtin_fminf(__builtin_fmaf(ul, bl, lo), __builtin_fmaf(ul, bh, lo)),
+                                               __builtin_fminf(__builtin_fmaf(uh, bl, lo), __builtin_fmaf(uh, bh, lo)));
+                    Mh[r][j] = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaf(ul, bl, hi), __builtin_fmaf(ul, bh, hi)),
+                                               __builtin_fmaxf(__builtin_fmaf(uh, bl, hi), __builtin_fmaf(uh, bh, hi)));
+                }
+            }
+    }
     __syncthreads();
     stamp(4);
-    dct2d_rows_layout<B, true>(x, tile, q);  // :204
+    idct2d_rows_layout_iv<B>(Ml, Mh, tile, tile2, q);  // :204
     stamp(5);
 
-    // :207-216 write back and ycbcr_to_rgb with this lane's original chroma
+    // :207-216 write back and ycbcr_to_rgb with this lane's original chroma: the lower ends'
+    // bytes; a pixel whose ends give other bytes leaves the block undecided
+    bool unc = neg;
     if (pos.valid && !slow) {
-        uint32_t words[R][NW];
-#pragma unroll
-        for (int r = 0; r < R; ++r)
-#pragma unroll
-            for (int i = 0; i < NW; ++i) words[r][i] = pix[r * NW + i][lane];
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             uint32_t out[Geo<B>::NW];
@@ -378,7 +508,13 @@ TMF_DEVI void embed_blocks(const EmbedArgs &a, const StripPos &pos, uint32_t id,
                 const uint32_t R0 = byte_at(words[r], 3 * c), G0 = byte_at(words[r], 3 * c + 1), B0 = byte_at(words[r], 3 * c + 2);
                 chroma(R0, G0, B0, cbs, crs);
                 uint32_t R8, G8, B8;
-                colour_inv(x[r][c], cbs, crs, R8, G8, B8);
+                colour_inv(Ml[r][c], cbs, crs, R8, G8, B8);
+                const bool wide = Ml[r][c] != Mh[r][c];
+                if (__builtin_amdgcn_ballot_w64(wide) != 0 && wide) {
+                    uint32_t R9, G9, B9;
+                    colour_inv(Mh[r][c], cbs, crs, R9, G9, B9);
+                    unc = unc || R9 != R8 || G9 != G8 || B9 != B8;
+                }
                 const int k0 = 3 * c;
                 out[k0 >> 2] |= R8 << (8 * (k0 & 3));
                 out[(k0 + 1) >> 2] |= G8 << (8 * ((k0 + 1) & 3));
@@ -388,15 +524,18 @@ TMF_DEVI void embed_blocks(const EmbedArgs &a, const StripPos &pos, uint32_t id,
             if (real_row<B>(q, r)) store_words<B>(p, a.aligned, out);
         }
     }
+    // the dgesdd route (embed_fixup_kernel) redoes flagged blocks and blocks with an undecided byte
+    const bool fix = flag20 || group_or<L>(unc && cert ? 1 : 0) != 0;
+    if (fix && pos.valid && !slow && q == 0) a.fb_list[atomicAdd(a.fb_count, 1u)] = id;
     stamp(6);
 }
 
 template <int B, bool LIST = false>
 __global__ __launch_bounds__(64, kEmbedWaves<B>) void embed_kernel(EmbedArgs a)
 {
-    constexpr int L = Geo<B>::L, R = Geo<B>::R, BPW = Geo<B>::BPW, NW = Geo<B>::NW, TS = kEmbedTS<B>;
-    __shared__ __attribute__((aligned(16))) float lds[BPW * TS];  // also svd3's scratch during the SVD
-    __shared__ uint32_t pix[R * NW][64];  // this lane's source bytes, parked during the SVD
+    constexpr int L = Geo<B>::L, BPW = Geo<B>::BPW, TS = kEmbedTS<B>;
+    __shared__ __attribute__((aligned(16))) float lds[BPW * TS];        // also svd3's scratch during the SVD
+    __shared__ __attribute__((aligned(16))) float lds2[kLds2Floats<B>];  // source bytes, then the upper-end tiles
     if constexpr (LIST) {
         // grid-stride over the slow list's segments (their lengths are known on the device only)
         const uint32_t per_frame = (uint32_t)a.nbh * (uint32_t)a.nbw, rows = (uint32_t)a.nframes * (uint32_t)a.nbh;
@@ -412,14 +551,14 @@ __global__ __launch_bounds__(64, kEmbedWaves<B>) void embed_kernel(EmbedArgs a)
                 const uint32_t rem = id % per_frame;
                 pos.bi = (int)(rem / (uint32_t)a.nbw);
                 pos.bj = (int)(rem % (uint32_t)a.nbw);
-                embed_blocks<B, true>(a, pos, id, lds, pix);
+                embed_blocks<B, true>(a, pos, id, lds, lds2);
                 __syncthreads();  // the LDS tiles are reused by the next listed blocks
             }
         }
     } else {
         const StripPos pos = strip_pos<B>(a.strips_per_row, a.nbw);
         const uint32_t id = (uint32_t)(((int64_t)blockIdx.y * a.nbh + pos.bi) * a.nbw + pos.bj);
-        embed_blocks<B, false>(a, pos, id, lds, pix);
+        embed_blocks<B, false>(a, pos, id, lds, lds2);
     }
 }
 

@@ -141,6 +141,20 @@ template <typename T> TMF_DEVI void colour_inv_t(T y, T cbs, T crs, uint32_t &R,
 // pocketfft fp32 DCT-II / DCT-III (N3), every even length 4..16, fully unrolled on
 // register arrays.  rfftp radix passes with compile-time (ido, l1).
 // ---------------------------------------------------------------------------
+// Interval of f32 values [lo, hi] for the hybrid route's byte certificate:
+// every operation below is the IEEE round-to-nearest operation on the end points, which is
+// monotone in each operand, so the result encloses every value the operation can produce
+// from operands inside the intervals (ends swapped by subtraction and negative constants).
+struct Ivf {
+    float lo, hi;
+};
+TMF_DEVI Ivf operator+(Ivf a, Ivf b) { return {a.lo + b.lo, a.hi + b.hi}; }
+TMF_DEVI Ivf operator-(Ivf a, Ivf b) { return {a.lo - b.hi, a.hi - b.lo}; }
+TMF_DEVI Ivf operator-(Ivf a) { return {-a.hi, -a.lo}; }
+TMF_DEVI Ivf operator*(float c, Ivf a) { return c >= 0.0f ? Ivf{c * a.lo, c * a.hi} : Ivf{c * a.hi, c * a.lo}; }
+TMF_DEVI Ivf operator*(Ivf a, float c) { return c * a; }
+TMF_DEVI Ivf &operator*=(Ivf &a, float c) { return a = c * a; }
+
 namespace dct {
 
 constexpr float kSqrt2 = 1.41421356237309504880f;
@@ -250,14 +264,14 @@ TMF_DEVI void radb4(const float (&cc)[N], float (&ch)[N], const float *wa)
 #undef CH
 }
 
-template <int IDO, int L1, int N>
-TMF_DEVI void radf2(const float (&cc)[N], float (&ch)[N], const float *wa)
+template <int IDO, int L1, int N, typename T>
+TMF_DEVI void radf2(const T (&cc)[N], T (&ch)[N], const float *wa)
 {
 #define CC(a, b, c) cc[(a) + IDO * ((b) + L1 * (c))]
 #define CH(a, b, c) ch[(a) + IDO * ((b) + 2 * (c))]
 #pragma unroll
     for (int k = 0; k < L1; k++) {
-        const float x = CC(0, k, 0), y = CC(0, k, 1);
+        const T x = CC(0, k, 0), y = CC(0, k, 1);
         CH(0, 0, k) = x + y;
         CH(IDO - 1, 1, k) = x - y;
     }
@@ -275,13 +289,13 @@ TMF_DEVI void radf2(const float (&cc)[N], float (&ch)[N], const float *wa)
             for (int i = 2; i < IDO; i += 2) {
                 const int ic = IDO - i;
                 const float w0 = wa[i - 2], w1 = wa[i - 1];
-                const float e = CC(i - 1, k, 1), f = CC(i, k, 1);
-                const float tr2 = w0 * e + w1 * f;
-                const float ti2 = w0 * f - w1 * e;
-                const float a = CC(i - 1, k, 0);
+                const T e = CC(i - 1, k, 1), f = CC(i, k, 1);
+                const T tr2 = w0 * e + w1 * f;
+                const T ti2 = w0 * f - w1 * e;
+                const T a = CC(i - 1, k, 0);
                 CH(i - 1, 0, k) = a + tr2;
                 CH(ic - 1, 1, k) = a - tr2;
-                const float c = CC(i, k, 0);
+                const T c = CC(i, k, 0);
                 CH(i, 0, k) = ti2 + c;
                 CH(ic, 1, k) = ti2 - c;
             }
@@ -290,18 +304,18 @@ TMF_DEVI void radf2(const float (&cc)[N], float (&ch)[N], const float *wa)
 #undef CH
 }
 
-template <int IDO, int L1, int N>
-TMF_DEVI void radf4(const float (&cc)[N], float (&ch)[N], const float *wa)
+template <int IDO, int L1, int N, typename T>
+TMF_DEVI void radf4(const T (&cc)[N], T (&ch)[N], const float *wa)
 {
 #define CC(a, b, c) cc[(a) + IDO * ((b) + L1 * (c))]
 #define CH(a, b, c) ch[(a) + IDO * ((b) + 4 * (c))]
 #pragma unroll
     for (int k = 0; k < L1; k++) {
-        float a = CC(0, k, 3), b = CC(0, k, 1);
-        const float tr1 = a + b;
+        T a = CC(0, k, 3), b = CC(0, k, 1);
+        const T tr1 = a + b;
         CH(0, 2, k) = a - b;
         a = CC(0, k, 0); b = CC(0, k, 2);
-        const float tr2 = a + b;
+        const T tr2 = a + b;
         CH(IDO - 1, 1, k) = a - b;
         CH(0, 0, k) = tr2 + tr1;
         CH(IDO - 1, 3, k) = tr2 - tr1;
@@ -309,12 +323,12 @@ TMF_DEVI void radf4(const float (&cc)[N], float (&ch)[N], const float *wa)
     if constexpr ((IDO & 1) == 0) {
 #pragma unroll
         for (int k = 0; k < L1; k++) {
-            const float ti1 = -kHsqt2 * (CC(IDO - 1, k, 1) + CC(IDO - 1, k, 3));
-            const float tr1 = kHsqt2 * (CC(IDO - 1, k, 1) - CC(IDO - 1, k, 3));
-            const float a = CC(IDO - 1, k, 0);
+            const T ti1 = -kHsqt2 * (CC(IDO - 1, k, 1) + CC(IDO - 1, k, 3));
+            const T tr1 = kHsqt2 * (CC(IDO - 1, k, 1) - CC(IDO - 1, k, 3));
+            const T a = CC(IDO - 1, k, 0);
             CH(IDO - 1, 0, k) = a + tr1;
             CH(IDO - 1, 2, k) = a - tr1;
-            const float c = CC(IDO - 1, k, 2);
+            const T c = CC(IDO - 1, k, 2);
             CH(0, 3, k) = ti1 + c;
             CH(0, 1, k) = ti1 - c;
         }
@@ -326,19 +340,19 @@ TMF_DEVI void radf4(const float (&cc)[N], float (&ch)[N], const float *wa)
             for (int i = 2; i < IDO; i += 2) {
                 const int ic = IDO - i;
                 float w0 = wa[i - 2], w1 = wa[i - 1];
-                float e = CC(i - 1, k, 1), f = CC(i, k, 1);
-                const float cr2 = w0 * e + w1 * f, ci2 = w0 * f - w1 * e;
+                T e = CC(i - 1, k, 1), f = CC(i, k, 1);
+                const T cr2 = w0 * e + w1 * f, ci2 = w0 * f - w1 * e;
                 w0 = wa[(IDO - 1) + i - 2]; w1 = wa[(IDO - 1) + i - 1];
                 e = CC(i - 1, k, 2); f = CC(i, k, 2);
-                const float cr3 = w0 * e + w1 * f, ci3 = w0 * f - w1 * e;
+                const T cr3 = w0 * e + w1 * f, ci3 = w0 * f - w1 * e;
                 w0 = wa[2 * (IDO - 1) + i - 2]; w1 = wa[2 * (IDO - 1) + i - 1];
                 e = CC(i - 1, k, 3); f = CC(i, k, 3);
-                const float cr4 = w0 * e + w1 * f, ci4 = w0 * f - w1 * e;
-                const float tr1 = cr4 + cr2, tr4 = cr4 - cr2;
-                const float ti1 = ci2 + ci4, ti4 = ci2 - ci4;
-                const float a = CC(i - 1, k, 0), c = CC(i, k, 0);
-                const float tr2 = a + cr3, tr3 = a - cr3;
-                const float ti2 = c + ci3, ti3 = c - ci3;
+                const T cr4 = w0 * e + w1 * f, ci4 = w0 * f - w1 * e;
+                const T tr1 = cr4 + cr2, tr4 = cr4 - cr2;
+                const T ti1 = ci2 + ci4, ti4 = ci2 - ci4;
+                const T a = CC(i - 1, k, 0), c = CC(i, k, 0);
+                const T tr2 = a + cr3, tr3 = a - cr3;
+                const T ti2 = c + ci3, ti3 = c - ci3;
                 CH(i - 1, 0, k) = tr2 + tr1;
                 CH(ic - 1, 3, k) = tr2 - tr1;
                 CH(i, 0, k) = ti1 + ti2;
@@ -447,25 +461,25 @@ TMF_DEVI void radbg(float (&cc)[N], float (&ch)[N], const float *cs)
     }
 }
 
-template <int L1, int N>
-TMF_DEVI void radf3(const float (&cc)[N], float (&ch)[N])
+template <int L1, int N, typename T>
+TMF_DEVI void radf3(const T (&cc)[N], T (&ch)[N])
 {
 #pragma unroll
     for (int k = 0; k < L1; k++) {
-        const float cr2 = cc[k + L1] + cc[k + 2 * L1];
+        const T cr2 = cc[k + L1] + cc[k + 2 * L1];
         ch[3 * k] = cc[k] + cr2;
         ch[2 + 3 * k] = kTaui * (cc[k + 2 * L1] - cc[k + L1]);
         ch[1 + 3 * k] = cc[k] + kTaur * cr2;
     }
 }
 
-template <int L1, int N>
-TMF_DEVI void radf5(const float (&cc)[N], float (&ch)[N])
+template <int L1, int N, typename T>
+TMF_DEVI void radf5(const T (&cc)[N], T (&ch)[N])
 {
 #pragma unroll
     for (int k = 0; k < L1; k++) {
-        const float cr2 = cc[k + 4 * L1] + cc[k + L1], ci5 = cc[k + 4 * L1] - cc[k + L1];
-        const float cr3 = cc[k + 3 * L1] + cc[k + 2 * L1], ci4 = cc[k + 3 * L1] - cc[k + 2 * L1];
+        const T cr2 = cc[k + 4 * L1] + cc[k + L1], ci5 = cc[k + 4 * L1] - cc[k + L1];
+        const T cr3 = cc[k + 3 * L1] + cc[k + 2 * L1], ci4 = cc[k + 3 * L1] - cc[k + 2 * L1];
         ch[5 * k] = cc[k] + cr2 + cr3;
         ch[5 * k + 1] = cc[k] + kTr11 * cr2 + kTr12 * cr3;
         ch[5 * k + 2] = kTi11 * ci5 + kTi12 * ci4;
@@ -475,8 +489,8 @@ TMF_DEVI void radf5(const float (&cc)[N], float (&ch)[N])
 }
 
 // generic odd radix, ido == 1: the result is left in cc (ch is scratch)
-template <int IP, int L1, int N>
-TMF_DEVI void radfg(float (&cc)[N], float (&ch)[N], const float *cs)
+template <int IP, int L1, int N, typename T>
+TMF_DEVI void radfg(T (&cc)[N], T (&ch)[N], const float *cs)
 {
     static_assert(IP <= 7, "accumulation tail restated for ip <= 7 only");
     constexpr int IPPH = (IP + 1) / 2;
@@ -485,7 +499,7 @@ TMF_DEVI void radfg(float (&cc)[N], float (&ch)[N], const float *cs)
         const int jc = IP - j;
 #pragma unroll
         for (int k = 0; k < L1; ++k) {
-            const float t1 = cc[k + L1 * j], t2 = cc[k + L1 * jc];
+            const T t1 = cc[k + L1 * j], t2 = cc[k + L1 * jc];
             cc[k + L1 * j] = t2 + t1;
             cc[k + L1 * jc] = t2 - t1;
         }
@@ -565,10 +579,10 @@ TMF_DEVI void rfft_backward(float (&c)[N], float fct)
     for (int i = 0; i < N; ++i) c[i] *= fct;
 }
 
-template <int N>
-TMF_DEVI void rfft_forward(float (&c)[N], float fct)
+template <int N, typename T>
+TMF_DEVI void rfft_forward(T (&c)[N], float fct)
 {
-    float ch[N];
+    T ch[N];
     if constexpr (N == 4) {
         radf4<1, 1>(c, ch, nullptr);
 #pragma unroll
@@ -639,8 +653,8 @@ TMF_DEVI void dct2(float (&c)[N])
 }
 
 // T_dcst23 type 3 (scipy.fftpack.idct, norm="ortho")
-template <int N>
-TMF_DEVI void dct3(float (&c)[N])
+template <int N, typename T>
+TMF_DEVI void dct3(T (&c)[N])
 {
     constexpr int NS2 = (N + 1) / 2;
     const float *tw = Tw<N>::d;
@@ -648,7 +662,7 @@ TMF_DEVI void dct3(float (&c)[N])
 #pragma unroll
     for (int k = 1; k < NS2; ++k) {
         const int kc = N - k;
-        const float t1 = c[k] + c[kc], t2 = c[k] - c[kc];
+        const T t1 = c[k] + c[kc], t2 = c[k] - c[kc];
         c[k] = tw[k - 1] * t2 + tw[kc - 1] * t1;
         c[kc] = tw[k - 1] * t1 - tw[kc - 1] * t2;
     }
@@ -656,7 +670,7 @@ TMF_DEVI void dct3(float (&c)[N])
     rfft_forward<N>(c, Tw<N>::norm);
 #pragma unroll
     for (int k = 1; k < N - 1; k += 2) {
-        const float t = c[k];
+        const T t = c[k];
         c[k] = t - c[k + 1];
         c[k + 1] = t + c[k + 1];
     }

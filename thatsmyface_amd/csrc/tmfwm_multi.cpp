@@ -132,11 +132,16 @@ int64_t pass_frames(int64_t frame_bytes)
 
 // Device staging buffers, kept per device across calls (an app batch loop calls the multi
 // entry points over and over; hipMalloc / hipFree of GiBs per call would cost more than a
-// pass).  A shard leases the buffers it needs and gives them back when it is done; the cache
-// holds them for the life of the process (at most two pass slots per concurrent shard).
+// pass).  A shard leases the buffers it needs and gives them back when it is done.  The cache
+// keeps at most kKeep free buffers per device (two pass slots of two shards); a lease takes the
+// smallest free buffer that fits and is at most twice the request (a small call does not hold a
+// GiB slot), and when hipMalloc fails it frees the device's cached buffers and tries once more.
+// tmfwm_release_cached_buffers() frees every cached buffer.
 struct BufCache {
+    static constexpr int kKeep = 4;
     std::mutex mu;
     std::multimap<int, std::pair<size_t, void *>> free;  // device -> (bytes, pointer)
+    std::map<void *, size_t> sizes;
     static BufCache &get()
     {
         static BufCache c;
@@ -147,17 +152,25 @@ struct BufCache {
         {
             std::lock_guard<std::mutex> lk(mu);
             auto r = free.equal_range(dev);
+            auto best = free.end();
             for (auto it = r.first; it != r.second; ++it)
-                if (it->second.first >= bytes) {
-                    void *p = it->second.second;
-                    free.erase(it);
-                    return p;
-                }
+                if (it->second.first >= bytes && it->second.first <= 2 * bytes &&
+                    (best == free.end() || it->second.first < best->second.first))
+                    best = it;
+            if (best != free.end()) {
+                void *p = best->second.second;
+                free.erase(best);
+                return p;
+            }
         }
         void *p = nullptr;
         if (hipMalloc(&p, bytes) != hipSuccess) {
             (void)hipGetLastError();
-            return nullptr;
+            release(dev);
+            if (hipMalloc(&p, bytes) != hipSuccess) {
+                (void)hipGetLastError();
+                return nullptr;
+            }
         }
         std::lock_guard<std::mutex> lk(mu);
         sizes[p] = bytes;
@@ -167,9 +180,31 @@ struct BufCache {
     {
         if (!p) return;
         std::lock_guard<std::mutex> lk(mu);
+        if ((int)free.count(dev) >= kKeep) {  // the oldest cached buffer of the device goes
+            auto it = free.find(dev);
+            (void)hipFree(it->second.second);
+            sizes.erase(it->second.second);
+            free.erase(it);
+        }
         free.emplace(dev, std::make_pair(sizes[p], p));
     }
-    std::map<void *, size_t> sizes;
+    // frees the cached (not leased) buffers of one device, or of every device (dev < 0)
+    int release(int dev)
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        int n = 0;
+        for (auto it = free.begin(); it != free.end();) {
+            if (dev >= 0 && it->first != dev) {
+                ++it;
+                continue;
+            }
+            (void)hipFree(it->second.second);
+            sizes.erase(it->second.second);
+            it = free.erase(it);
+            ++n;
+        }
+        return n;
+    }
 };
 
 int plan_shards(const int32_t *devices, int32_t n_shards, int64_t n_frames, std::vector<Shard> &sh, std::vector<DeviceTile> &uniq)
@@ -511,6 +546,8 @@ int tmfwm_extract_multi_route(const uint8_t *wm_rgb, const uint8_t *orig_rgb, in
     }
     return join(sh, th, n_lapack_blocks);
 }
+
+int tmfwm_release_cached_buffers(void) { return BufCache::get().release(-1); }
 
 int tmfwm_embed_multi(const uint8_t *rgb, int64_t n_frames, int32_t height, int32_t width, int64_t frame_stride,
                       const uint8_t *wm_tile, int32_t block, double alpha, uint8_t *out, const int32_t *devices,

@@ -73,3 +73,8 @@ def extract_multi(wframes: np.ndarray, oframes: np.ndarray, block: int = 8, alph
     if stats is not None:
         stats["lapack_blocks"] = int(cnt.value)
     return out
+
+
+def release_cached_buffers() -> int:
+    """Frees the device staging buffers the multi-GPU calls keep between calls (tmfwm_release_cached_buffers)."""
+    return int(_lib.load().tmfwm_release_cached_buffers())

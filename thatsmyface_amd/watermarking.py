@@ -24,6 +24,7 @@ import io
 import os
 import sys
 import threading
+import weakref
 
 import numpy as np
 from PIL import Image
@@ -199,12 +200,19 @@ _zero_copy = os.environ.get("TMFWM_PIL_ZERO_COPY", "1") != "0"
 _pa = None
 _POOL_KEEP = 4  # output buffers kept per size
 _out_pool: "dict[int, list[np.ndarray]]" = {}
+_out_free: "set[int]" = set()  # ids of pooled buffers whose image has been collected
 _pool_lock = threading.Lock()
 
 
 def _arrow():
+    """pyarrow when the zero-copy path can run: it also needs Pillow's Arrow interface
+    (Image.fromarrow and Image.__arrow_c_array__, Pillow >= 11.2; the reference asks for
+    Pillow >= 9, requirements.txt:3), otherwise every call takes the copying path."""
     global _pa, _zero_copy
     if _pa is None and _zero_copy:
+        if not (hasattr(Image, "fromarrow") and hasattr(Image.Image, "__arrow_c_array__")):
+            _zero_copy = False
+            return None
         try:
             import pyarrow  # noqa: PLC0415
 
@@ -232,13 +240,23 @@ def _rgbx_view(image):
     return vals.buffers()[1].address + vals.offset, arr
 
 
+def _release(buf: np.ndarray) -> None:
+    with _pool_lock:
+        if any(b is buf for b in _out_pool.get(buf.size, ())):  # pooled: free for the next call
+            _out_free.add(id(buf))
+
+
 def _take_out(nbytes: int) -> np.ndarray:
-    """An RGBX output buffer: a pooled one nothing else references (its image is gone), else new
-    (its pages are then faulted in once; page-locked buffers measured no faster, r04k)."""
+    """An RGBX output buffer: a pooled one whose image has been collected (weakref.finalize on
+    the image, _rgb_from_rgbx) and that nothing else still references, else a new one (its pages
+    are then faulted in once; page-locked buffers measured no faster, r04k)."""
     with _pool_lock:
         lst = _out_pool.setdefault(nbytes, [])
         for b in lst:
-            if sys.getrefcount(b) == 3:  # the list, this loop's name and the call's argument
+            # the finalizer is the signal; the reference count only vetoes (an Arrow export of
+            # the image taken by the caller keeps the buffer: the list, this name, the argument)
+            if id(b) in _out_free and sys.getrefcount(b) <= 3:
+                _out_free.discard(id(b))
                 return b
         b = np.empty(nbytes, np.uint8)
         if len(lst) < _POOL_KEEP:
@@ -252,6 +270,7 @@ def _rgb_from_rgbx(buf: np.ndarray, width: int, height: int):
     vals = pa.Array.from_buffers(pa.uint8(), width * height * 4, [None, pa.py_buffer(buf)])
     img = Image.fromarrow(pa.FixedSizeListArray.from_arrays(vals, 4), "RGB", (width, height))
     img._tmfwm_rgbx = buf  # extract_watermark reads it back without an export
+    weakref.finalize(img, _release, buf)  # the pool may hand the buffer out again
     return img
 
 

@@ -99,8 +99,20 @@ def main():
     for kind in os.environ.get("KINDS", "noise,photo").split(","):
         for f in range(n):
             t0 = time.time()
-            cov = O.synth_bytes(0x5EED0001, f, 1, H * W * 3).reshape(H, W, 3) if kind == "noise" else photo_cover(H, W, 100 + f)
-            tile = O.synth_bytes(0x5EED0002, 0, 1, (H // b) * (W // b)).reshape(H // b, W // b)
+            if kind == "noise":
+                cov = O.synth_bytes(0x5EED0001, f, 1, H * W * 3).reshape(H, W, 3)
+            elif kind == "photo":
+                cov = photo_cover(H, W, 100 + f)
+            else:
+                from golden.gen_golden import cover
+                cov = cover(kind, H, W, 11 + f)
+                if cov.ndim == 2:
+                    cov = np.stack([cov] * 3, -1)
+            if os.environ.get("WM") == "qr":
+                from golden.gen_golden import wmark
+                tile = wmark("qr", H // b, W // b, 3 + f)
+            else:
+                tile = O.synth_bytes(0x5EED0002, 0, 1, (H // b) * (W // b)).reshape(H // b, W // b)
             r = study(L, cov, tile, b, alpha, Ks)
             print(kind, f, f"{time.time() - t0:.1f}s", r, flush=True)
 

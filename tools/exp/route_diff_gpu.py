@@ -44,6 +44,13 @@ def photo_covers(n, H, W, seed, dev):
     return img.clamp_(0, 255).to(torch.uint8)
 
 
+def qr_tile(nbh, nbw, seed, dev):
+    """Binary 0 / 255 watermark tile (a resized QR code's modules at one pixel per block)."""
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed + 99)
+    return torch.randint(0, 2, (nbh, nbw), generator=g, device=dev, dtype=torch.uint8) * 255
+
+
 def blocks_differing(a, c, b):
     """Blocks of (n, H, W, 3) frames holding at least one differing byte."""
     n, H, W, _ = a.shape
@@ -61,10 +68,12 @@ def main():
     p.add_argument("--height", type=int, default=2160)
     p.add_argument("--width", type=int, default=3840)
     p.add_argument("--seed", type=int, default=1)
+    p.add_argument("--wm", choices=["noise", "qr"], default="noise",
+                   help="watermark tile: uniform bytes (the bench's) or binary 0 / 255 (a QR code, the app's)")
     a = p.parse_args()
     dev = torch.device("cuda", 0)
     H, W, b = a.height, a.width, a.block
-    tile = batch.synth_tile(H // b, W // b, device=dev)
+    tile = qr_tile(H // b, W // b, a.seed, dev) if a.wm == "qr" else batch.synth_tile(H // b, W // b, device=dev)
     tot = dict(frames=0, blocks=0, dgesdd_route_blocks=0, embed_bytes_differing=0, embed_blocks_differing=0,
                extract_bytes_differing=0, extract_same_input_bytes_differing=0)
     t_start = time.time()
@@ -89,7 +98,7 @@ def main():
             tot[k] += row[k]
         print(json.dumps(row), flush=True)
         del fr, oh, orf, xh, xr, xs
-    tot.update(block=b, kind=a.kind, frame=f"{W}x{H}", alpha=a.alpha, seconds=round(time.time() - t_start, 1))
+    tot.update(block=b, kind=a.kind, wm=a.wm, frame=f"{W}x{H}", alpha=a.alpha, seconds=round(time.time() - t_start, 1))
     print(json.dumps({"total": tot}), flush=True)
 
 

@@ -22,12 +22,18 @@ def main():
     p.add_argument("--frames", type=int, default=128)
     p.add_argument("--block", type=int, default=8)
     p.add_argument("--reps", type=int, default=3)
+    p.add_argument("--kind", choices=["noise", "photo"], default="noise", help="covers: the bench's noise or camera-like")
+    p.add_argument("--wm", choices=["noise", "qr"], default="noise", help="watermark tile: uniform bytes or binary (QR)")
     a = p.parse_args()
     dev = torch.device("cuda", 0)
     b = a.block
-    fr = batch.synth_frames(a.frames, 2160, 3840, device=dev)
-    tile = batch.synth_tile(2160 // b, 3840 // b, device=dev)
-    out = batch.embed_batch(fr, tile, b, 0.1)
+    sys.path.insert(0, os.path.join(ROOT, "tools", "exp"))
+    from route_diff_gpu import photo_covers, qr_tile
+
+    fr = photo_covers(a.frames, 2160, 3840, 5, dev) if a.kind == "photo" else batch.synth_frames(a.frames, 2160, 3840, device=dev)
+    tile = qr_tile(2160 // b, 3840 // b, 1, dev) if a.wm == "qr" else batch.synth_tile(2160 // b, 3840 // b, device=dev)
+    st = {}
+    out = batch.embed_batch(fr, tile, b, 0.1, stats=st)
     ext = batch.extract_batch(out, fr, b, 0.1)
     torch.cuda.synchronize()
     res = {}
@@ -40,7 +46,8 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         res[name] = round(e0.elapsed_time(e1) * 1000 / a.reps / a.frames, 2)
-    print(json.dumps({"lib": os.path.basename(os.environ.get("TMFWM_LIB", "libtmfwm.so")), "block": b, "us_per_frame": res}))
+    print(json.dumps({"lib": os.path.basename(os.environ.get("TMFWM_LIB", "libtmfwm.so")), "block": b, "kind": a.kind, "wm": a.wm,
+                      "frames": a.frames, "dgesdd_route_blocks": st.get("lapack_blocks"), "us_per_frame": res}))
 
 
 if __name__ == "__main__":
