@@ -68,7 +68,7 @@ def lib():
             "orc_embed_frame_mode": (I32, [_u8p, I32, I32, _u8p, I32, D, _u8p, I32, I32, ctypes.POINTER(I64)]),
             "orc_extract_frame_mode": (I32, [_u8p, _u8p, I32, I32, I32, D, _u8p, I32, I32]),
             "orc_svd_flag": (I32, [_f64p, I32]),
-            "orc_cert_block": (I32, [_f64p, _f64p, _f64p, I32, ctypes.c_uint8, D, _f32p, _f32p, ctypes.POINTER(I64)]),
+            "orc_cert_block": (I32, [_f32p, _f64p, _f64p, _f64p, I32, ctypes.c_uint8, D, _f32p, _f32p, ctypes.POINTER(I64)]),
             "orc_cert_idct_point": (None, [_f32p, I32]),
             "orc_rsq_hw": (ctypes.c_float, [ctypes.c_float]),
             "orc_svd_blocks_f64": (None, [_f32p, I64, I32, _f64p, _f64p, _f64p, I32]),

@@ -22,7 +22,7 @@ const dct_plan *orc_plan(int n);                                     /* n = 4, 6
 void orc_colour_inv_px(float y, float cbs, float crs, uint8_t out[3]); /* N9 for one pixel */
 
 /* tmfwm_cert.cpp: the hybrid route's byte certificate */
-int orc_cert_block(const double *U, const double *sig, const double *V, int b, uint8_t w, double alpha,
+int orc_cert_block(const float *D, const double *U, const double *sig, const double *V, int b, uint8_t w, double alpha,
                    const float *cbs, const float *crs, int64_t *stats);
 
 #ifdef __cplusplus

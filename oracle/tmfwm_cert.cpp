@@ -20,8 +20,16 @@
  *
  * Contract (the device's embed_kernel computes the same end points bit for bit):
  *   s1 = max sigma_k; s1 == 0: certain (zero block, N6);
+ *   D zero but for D[0][0] (a flat block): certain -- dgebd2's reflectors are identities
+ *     (tau = 0), dbdsqr only makes d_1 positive: U = I, S = |d|, Vt = diag(sgn d, 1, ..) in
+ *     LAPACK, U e_0 = sgn(d) e_0, V = I here, and every other product of the chain is a zero
+ *     added to +0, so both routes' M are the same bits;
+ *   uncertain (the dgesdd route) when some rank has an interval containing 0 (lo < 0 < hi) on
+ *     one side of the product (its U column or its Bm row) and a non-point interval on the
+ *     other: the device's end-point selection is exact unless both hold (exact zeros of
+ *     structured blocks);
  *   keep_k = f32(sigma_k) != 0, g_k = min(sigma_k, min_{j != k} |sigma_k - sigma_j|),
- *   E_k = (2^-45 s1) / g_k (keep_k), Es = 2^-45 s1;
+ *   E_k = t / g_k (keep_k; t = 2^-45 s1), Es = t;
  *   S_k in [f32(max(sigma_k - Es, 0)), f32(sigma_k + Es)]; S'_0 ends f32(f64(end) + c);
  *   keep_k:  U_rk in [f32(u - E_k), f32(u + E_k)], V_jk likewise, B_kj = S'_k x V_jk
  *            (S' >= 0: lo = S'lo v_lo if v_lo >= 0 else S'hi v_lo; hi = S'lo v_hi if
@@ -271,12 +279,15 @@ const double kCertScale = 0x1p-45; /* K 2^-53, K = 256 */
 
 }  // namespace
 
-extern "C" int orc_cert_block(const double *U, const double *sig, const double *V, int b, uint8_t w, double alpha,
-                              const float *cbs, const float *crs, int64_t *stats)
+extern "C" int orc_cert_block(const float *D, const double *U, const double *sig, const double *V, int b, uint8_t w,
+                              double alpha, const float *cbs, const float *crs, int64_t *stats)
 {
     double s1 = 0.0;
     for (int k = 0; k < b; ++k) s1 = sig[k] > s1 ? sig[k] : s1;
     if (s1 == 0.0) return 0;
+    int dc_only = 1;
+    for (int i = 1; i < b * b; ++i) dc_only &= D[i] == 0.0f;
+    if (dc_only) return 0;
     const double t = kCertScale * s1, Es = t;
     Iv S[16], Ui[16][16], Bi[16][16];
     for (int k = 0; k < b; ++k) {
@@ -308,6 +319,16 @@ extern "C" int orc_cert_block(const double *U, const double *sig, const double *
             const float vl = (float)(v - E), vh = (float)(v + E);
             Bi[k][j] = {vl >= 0.0f ? S[k].lo * vl : S[k].hi * vl, vh <= 0.0f ? S[k].lo * vh : S[k].hi * vh};
         }
+    }
+    for (int k = 0; k < b; ++k) {
+        int ustr = 0, uwide = 0, bstr = 0, bwide = 0;
+        for (int r = 0; r < b; ++r) {
+            ustr |= Ui[r][k].lo < 0.0f && Ui[r][k].hi > 0.0f;
+            uwide |= Ui[r][k].lo != Ui[r][k].hi;
+            bstr |= Bi[k][r].lo < 0.0f && Bi[k][r].hi > 0.0f;
+            bwide |= Bi[k][r].lo != Bi[k][r].hi;
+        }
+        if ((ustr && bwide) || (bstr && uwide)) return 1;
     }
     Iv M[16][16];
     int64_t munc = 0, yunc = 0;

@@ -1123,7 +1123,7 @@ static int svd_block_route(const float *D, int b, int mode, float *U, float *S, 
     double U64[ORC_MAXB * ORC_MAXB], V64[ORC_MAXB * ORC_MAXB], sig[ORC_MAXB];
     orc_svd_block_f64(D, b, U64, sig, V64);
     if (mode == ORC_SVD_HYBRID &&
-        (orc_svd_flag(sig, b) || (cbs && orc_cert_block(U64, sig, V64, b, w, alpha, cbs, crs, NULL)))) {
+        (orc_svd_flag(sig, b) || (cbs && orc_cert_block(D, U64, sig, V64, b, w, alpha, cbs, crs, NULL)))) {
         orc_lp_svd_block_f32(D, b, U, S, Vt);
         return 1;
     }

@@ -295,6 +295,14 @@ TMF_DEVI void embed_blocks(const EmbedArgs &a, const StripPos &pos, uint32_t id,
     }
     dct2d_rows_layout<B, false>(x, tile, q);  // :192
     stamp(0);
+    // a flat block (D zero but for D[0][0]) has the same factors on both routes (oracle tmfwm_cert.cpp)
+    int ac = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int c = 0; c < B; ++c)
+            if (r > 0 || c > 0 || q > 0) ac |= x[r][c] != 0.0f ? 1 : 0;
+    const bool flat = group_or<L>(ac) == 0;
 
     double A[R][B], V[R][B];
     // :195 (SVD); svd3's scratch and (b = 16) the parked D in the block's tile
@@ -346,7 +354,7 @@ TMF_DEVI void embed_blocks(const EmbedArgs &a, const StripPos &pos, uint32_t id,
     const bool flag20 = m * 1048576.0 < s1;
     // Byte certificate: the interval bounds of the blocks whose bytes it decides (zero,
     // flagged and deferred blocks keep point intervals: the point path's values)
-    const bool cert = !zero && !flag20 && !slow;
+    const bool cert = !zero && !flat && !flag20 && !slow;
     const double tE = cert ? kCertScale * s1 : 0.0;
     double E[B];
     bool keep[B];
@@ -388,7 +396,8 @@ TMF_DEVI void embed_blocks(const EmbedArgs &a, const StripPos &pos, uint32_t id,
     }
     // U = A / sigma as f32 intervals [f32(u - E), f32(u + E)]; triplets that do not reach the
     // output (f32(sigma) == 0) take U = [2, 2] against B = [-2 S', 2 S'] (|f32 entries| <= 1)
-    bool straddle = false;  // an interval of a triplet that reaches the output contains 0
+    // per rank, over this lane's rows: U / Bm intervals that contain 0, and that are not points
+    unsigned ustr = 0, uwide = 0, bstr = 0, bwide = 0;
 #pragma unroll
     for (int k = 0; k < B; ++k) {
         const double inv = 1.0 / sig[k];
@@ -403,8 +412,8 @@ TMF_DEVI void embed_blocks(const EmbedArgs &a, const StripPos &pos, uint32_t id,
                 const double u = A[r][k] * inv;
                 ul = (float)(u - E[k]);
                 uh = (float)(u + E[k]);
-                straddle = straddle || (ul < 0.0f && uh > 0.0f);
             }
+
             if (real_row<B>(q, r)) {
                 tile[(q * R + r) * LD + rk[k]] = ul;
                 tile2[(q * R + r) * LD + rk[k]] = uh;
@@ -419,6 +428,8 @@ TMF_DEVI void embed_blocks(const EmbedArgs &a, const StripPos &pos, uint32_t id,
         for (int t = 0; t < B; ++t) {
             Ul[r][t] = real_row<B>(q, r) ? tile[(q * R + r) * LD + t] : 0.0f;
             Uh[r][t] = real_row<B>(q, r) ? tile2[(q * R + r) * LD + t] : 0.0f;
+            ustr |= (Ul[r][t] < 0.0f && Uh[r][t] > 0.0f ? 1u : 0u) << t;
+            uwide |= (Ul[r][t] != Uh[r][t] ? 1u : 0u) << t;
         }
     __syncthreads();
 
@@ -436,9 +447,12 @@ TMF_DEVI void embed_blocks(const EmbedArgs &a, const StripPos &pos, uint32_t id,
                 bh = 2.0f * Sh[k];
             } else {
                 const float vl = (float)(V[r][k] - E[k]), vh = (float)(V[r][k] + E[k]);
-                straddle = straddle || (vl < 0.0f && vh > 0.0f);
                 bl = vl >= 0.0f ? Sl[k] * vl : Sh[k] * vl;
                 bh = vh <= 0.0f ? Sl[k] * vh : Sh[k] * vh;
+            }
+            if (real_row<B>(q, r)) {  // by triplet here, by rank below
+                bstr |= (bl < 0.0f && bh > 0.0f ? 1u : 0u) << k;
+                bwide |= (bl != bh ? 1u : 0u) << k;
             }
             if (real_row<B>(q, r)) {
                 tile[rk[k] * LD + q * R + r] = bl;
@@ -452,42 +466,41 @@ TMF_DEVI void embed_blocks(const EmbedArgs &a, const StripPos &pos, uint32_t id,
     // profiles/r04/r04b).  Every M[r][j] is the fma chain over k = 0..b-1; on intervals, the
     // lower end takes the corner of the smallest product: u's lower end if b >= 0, else its
     // upper one, and b's lower end if u >= 0, else its upper one (exact when neither interval
-    // contains 0, or one of them is a point; otherwise the wave takes all four corners).
+    // contains 0, or one of them is a point; blocks where neither holds take the dgesdd route).
     float Ml[R][B], Mh[R][B];
 #pragma unroll
     for (int r = 0; r < R; ++r)
 #pragma unroll
         for (int j = 0; j < B; ++j) Ml[r][j] = Mh[r][j] = 0.0f;
-    if (__builtin_amdgcn_ballot_w64(straddle && cert) == 0) {
+    // The end-point selection is exact unless a rank has an interval containing 0 on one side of
+    // the product and a non-point interval on the other (exact zeros of structured blocks): such a
+    // block goes to the dgesdd route (oracle tmfwm_cert.cpp)
+    {
+        unsigned sr = 0, wr = 0;
 #pragma unroll
-        for (int k = 0; k < B; ++k)
-#pragma unroll
-            for (int j = 0; j < B; ++j) {
-                const float bl = tile[k * LD + j], bh = tile2[k * LD + j];
-                const bool bp = bl >= 0.0f;
-#pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    const bool up = Ul[r][k] >= 0.0f;
-                    Ml[r][j] = __builtin_fmaf(bp ? Ul[r][k] : Uh[r][k], up ? bl : bh, Ml[r][j]);
-                    Mh[r][j] = __builtin_fmaf(bp ? Uh[r][k] : Ul[r][k], up ? bh : bl, Mh[r][j]);
-                }
-            }
-    } else {
-#pragma unroll
-        for (int k = 0; k < B; ++k)
-#pragma unroll
-            for (int j = 0; j < B; ++j) {
-                const float bl = tile[k * LD + j], bh = tile2[k * LD + j];
-#pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    const float ul = Ul[r][k], uh = Uh[r][k], lo = Ml[r][j], hi = Mh[r][j];
-                    Ml[r][j] = __builtin_fminf(__builtin_fminf(__builtin_fmaf(ul, bl, lo), __builtin_fmaf(ul, bh, lo)),
-                                               __builtin_fminf(__builtin_fmaf(uh, bl, lo), __builtin_fmaf(uh, bh, lo)));
-                    Mh[r][j] = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaf(ul, bl, hi), __builtin_fmaf(ul, bh, hi)),
-                                               __builtin_fmaxf(__builtin_fmaf(uh, bl, hi), __builtin_fmaf(uh, bh, hi)));
-                }
-            }
+        for (int k = 0; k < B; ++k) {
+            sr |= ((bstr >> k) & 1u) << rk[k];
+            wr |= ((bwide >> k) & 1u) << rk[k];
+        }
+        bstr = sr;
+        bwide = wr;
     }
+    const int ub = (int)(ustr | (uwide << 16)), bb = (int)(bstr | (bwide << 16));
+    const unsigned gu = (unsigned)group_or<L>(ub), gb = (unsigned)group_or<L>(bb);
+    const bool mixed = ((gu & 0xFFFFu) & (gb >> 16)) != 0 || ((gb & 0xFFFFu) & (gu >> 16)) != 0;
+#pragma unroll
+    for (int k = 0; k < B; ++k)
+#pragma unroll
+        for (int j = 0; j < B; ++j) {
+            const float bl = tile[k * LD + j], bh = tile2[k * LD + j];
+            const bool bp = bl >= 0.0f;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const bool up = Ul[r][k] >= 0.0f;
+                Ml[r][j] = __builtin_fmaf(bp ? Ul[r][k] : Uh[r][k], up ? bl : bh, Ml[r][j]);
+                Mh[r][j] = __builtin_fmaf(bp ? Uh[r][k] : Ul[r][k], up ? bh : bl, Mh[r][j]);
+            }
+        }
     __syncthreads();
     stamp(4);
     idct2d_rows_layout_iv<B>(Ml, Mh, tile, tile2, q);  // :204
@@ -525,7 +538,7 @@ TMF_DEVI void embed_blocks(const EmbedArgs &a, const StripPos &pos, uint32_t id,
         }
     }
     // the dgesdd route (embed_fixup_kernel) redoes flagged blocks and blocks with an undecided byte
-    const bool fix = flag20 || group_or<L>(unc && cert ? 1 : 0) != 0;
+    const bool fix = flag20 || (cert && mixed) || group_or<L>(unc && cert ? 1 : 0) != 0;
     if (fix && pos.valid && !slow && q == 0) a.fb_list[atomicAdd(a.fb_count, 1u)] = id;
     stamp(6);
 }
