@@ -24,10 +24,10 @@
  *     (tau = 0), dbdsqr only makes d_1 positive: U = I, S = |d|, Vt = diag(sgn d, 1, ..) in
  *     LAPACK, U e_0 = sgn(d) e_0, V = I here, and every other product of the chain is a zero
  *     added to +0, so both routes' M are the same bits;
- *   uncertain (the dgesdd route) when some rank has an interval containing 0 (lo < 0 < hi) on
- *     one side of the product (its U column or its Bm row) and a non-point interval on the
- *     other: the device's end-point selection is exact unless both hold (exact zeros of
- *     structured blocks);
+ *   uncertain (the dgesdd route) when an element interval of a triplet that reaches the output
+ *     contains 0 (lo < 0 < hi) and some element interval of the block is not a point: the
+ *     device's end-point selection is exact unless a rank has both on the two sides of the
+ *     product, and this block-level test covers that (exact zeros of structured blocks);
  *   keep_k = f32(sigma_k) != 0, g_k = min(sigma_k, min_{j != k} |sigma_k - sigma_j|),
  *   E_k = t / g_k (keep_k; t = 2^-45 s1), Es = t;
  *   S_k in [f32(max(sigma_k - Es, 0)), f32(sigma_k + Es)]; S'_0 ends f32(f64(end) + c);
@@ -320,16 +320,14 @@ extern "C" int orc_cert_block(const float *D, const double *U, const double *sig
             Bi[k][j] = {vl >= 0.0f ? S[k].lo * vl : S[k].hi * vl, vh <= 0.0f ? S[k].lo * vh : S[k].hi * vh};
         }
     }
-    for (int k = 0; k < b; ++k) {
-        int ustr = 0, uwide = 0, bstr = 0, bwide = 0;
+    int str = 0, wid = 0; /* over the triplets that reach the output */
+    for (int k = 0; k < b; ++k)
         for (int r = 0; r < b; ++r) {
-            ustr |= Ui[r][k].lo < 0.0f && Ui[r][k].hi > 0.0f;
-            uwide |= Ui[r][k].lo != Ui[r][k].hi;
-            bstr |= Bi[k][r].lo < 0.0f && Bi[k][r].hi > 0.0f;
-            bwide |= Bi[k][r].lo != Bi[k][r].hi;
+            wid |= Ui[r][k].lo != Ui[r][k].hi || Bi[k][r].lo != Bi[k][r].hi;
+            if ((float)sig[k] != 0.0f)
+                str |= (Ui[r][k].lo < 0.0f && Ui[r][k].hi > 0.0f) || (Bi[k][r].lo < 0.0f && Bi[k][r].hi > 0.0f);
         }
-        if ((ustr && bwide) || (bstr && uwide)) return 1;
-    }
+    if (str && wid) return 1;
     Iv M[16][16];
     int64_t munc = 0, yunc = 0;
     for (int i = 0; i < b; ++i)

@@ -228,7 +228,7 @@ TMF_DEVI void luma_rows(const uint32_t (&words)[Geo<B>::R][Geo<B>::NW], float (&
 // one wave per SIMD).  Forcing 2 for b = 12 / 16 costs 156 / 256 B of scratch per lane
 // and is faster: embed<12> 283 -> 201 us, embed<16> 531 -> 345 us per 4K frame.
 template <int B>
-constexpr int kEmbedWaves = (B == 8 || B == 12 || B == 14 || B == 16) ? 2 : 1;
+constexpr int kEmbedWaves = (B == 8 || B == 10 || B == 12 || B == 16) ? 2 : 1;
 
 // Strip pass: once at most kDeferMax blocks of a wave still need f64 sweeps after a sweep
 // and its Newton try, the wave leaves them to the list pass instead of running another
@@ -267,6 +267,11 @@ template <int B>
 constexpr int kHiTile = B * (B + 1);
 template <int B>
 constexpr int kLds2Floats = kPixWords<B> > Geo<B>::BPW * kHiTile<B> ? kPixWords<B> : Geo<B>::BPW * kHiTile<B>;
+
+// The reconstruction picks each row's b end by an LDS offset (b = 8, 16) or by value selects
+// (the other sizes, where the offset form costs registers)
+template <int B>
+constexpr bool kOffsetPick = B == 8 || B == 16;
 
 // One wave's blocks: strip mode (LIST = false: the strip of blockIdx) or list mode (pos and
 // id from the slow list).  id = (frame * nbh + bi) * nbw + bj, relative to a.src.
@@ -396,8 +401,9 @@ TMF_DEVI void embed_blocks(const EmbedArgs &a, const StripPos &pos, uint32_t id,
     }
     // U = A / sigma as f32 intervals [f32(u - E), f32(u + E)]; triplets that do not reach the
     // output (f32(sigma) == 0) take U = [2, 2] against B = [-2 S', 2 S'] (|f32 entries| <= 1)
-    // per rank, over this lane's rows: U / Bm intervals that contain 0, and that are not points
-    unsigned ustr = 0, uwide = 0, bstr = 0, bwide = 0;
+    // over this lane's rows of the triplets that reach the output: an interval that contains 0,
+    // an interval that is not a point
+    int str = 0, wid = 0;
 #pragma unroll
     for (int k = 0; k < B; ++k) {
         const double inv = 1.0 / sig[k];
@@ -428,8 +434,8 @@ TMF_DEVI void embed_blocks(const EmbedArgs &a, const StripPos &pos, uint32_t id,
         for (int t = 0; t < B; ++t) {
             Ul[r][t] = real_row<B>(q, r) ? tile[(q * R + r) * LD + t] : 0.0f;
             Uh[r][t] = real_row<B>(q, r) ? tile2[(q * R + r) * LD + t] : 0.0f;
-            ustr |= (Ul[r][t] < 0.0f && Uh[r][t] > 0.0f ? 1u : 0u) << t;
-            uwide |= (Ul[r][t] != Uh[r][t] ? 1u : 0u) << t;
+            str |= (int)(Ul[r][t] < 0.0f) & (int)(Uh[r][t] > 0.0f);
+            wid |= (int)(Ul[r][t] != Uh[r][t]);
         }
     __syncthreads();
 
@@ -450,11 +456,9 @@ TMF_DEVI void embed_blocks(const EmbedArgs &a, const StripPos &pos, uint32_t id,
                 bl = vl >= 0.0f ? Sl[k] * vl : Sh[k] * vl;
                 bh = vh <= 0.0f ? Sl[k] * vh : Sh[k] * vh;
             }
-            if (real_row<B>(q, r)) {  // by triplet here, by rank below
-                bstr |= (bl < 0.0f && bh > 0.0f ? 1u : 0u) << k;
-                bwide |= (bl != bh ? 1u : 0u) << k;
-            }
             if (real_row<B>(q, r)) {
+                str |= (int)keep[k] & (int)(bl < 0.0f) & (int)(bh > 0.0f);
+                wid |= (int)(bl != bh);
                 tile[rk[k] * LD + q * R + r] = bl;
                 tile2[rk[k] * LD + q * R + r] = bh;
             }
@@ -472,35 +476,49 @@ TMF_DEVI void embed_blocks(const EmbedArgs &a, const StripPos &pos, uint32_t id,
     for (int r = 0; r < R; ++r)
 #pragma unroll
         for (int j = 0; j < B; ++j) Ml[r][j] = Mh[r][j] = 0.0f;
-    // The end-point selection is exact unless a rank has an interval containing 0 on one side of
-    // the product and a non-point interval on the other (exact zeros of structured blocks): such a
-    // block goes to the dgesdd route (oracle tmfwm_cert.cpp)
-    {
-        unsigned sr = 0, wr = 0;
+    // The end-point selection is exact unless some rank has an interval containing 0 on one side of
+    // the product and a non-point interval on the other (exact zeros of structured blocks); a block
+    // with an interval containing 0 and a non-point interval anywhere goes to the dgesdd route
+    // (oracle tmfwm_cert.cpp: the same block-level test)
+    const bool mixed = (group_or<L>(str) & group_or<L>(wid)) != 0;
+    // b's end for each row comes from the LDS tile the row's u sign picks (an offset select per
+    // row and rank instead of a value select per element; both tiles live in one LDS array)
+    const int dt = (int)(tile2 - tile);
+    if constexpr (kOffsetPick<B>) {
 #pragma unroll
-        for (int k = 0; k < B; ++k) {
-            sr |= ((bstr >> k) & 1u) << rk[k];
-            wr |= ((bwide >> k) & 1u) << rk[k];
+    for (int k = 0; k < B; ++k) {
+        int ol[R], oh[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const bool up = Ul[r][k] >= 0.0f;
+            ol[r] = up ? 0 : dt;
+            oh[r] = up ? dt : 0;
         }
-        bstr = sr;
-        bwide = wr;
-    }
-    const int ub = (int)(ustr | (uwide << 16)), bb = (int)(bstr | (bwide << 16));
-    const unsigned gu = (unsigned)group_or<L>(ub), gb = (unsigned)group_or<L>(bb);
-    const bool mixed = ((gu & 0xFFFFu) & (gb >> 16)) != 0 || ((gb & 0xFFFFu) & (gu >> 16)) != 0;
-#pragma unroll
-    for (int k = 0; k < B; ++k)
 #pragma unroll
         for (int j = 0; j < B; ++j) {
-            const float bl = tile[k * LD + j], bh = tile2[k * LD + j];
-            const bool bp = bl >= 0.0f;
+            const bool bp = tile[k * LD + j] >= 0.0f;
 #pragma unroll
             for (int r = 0; r < R; ++r) {
-                const bool up = Ul[r][k] >= 0.0f;
-                Ml[r][j] = __builtin_fmaf(bp ? Ul[r][k] : Uh[r][k], up ? bl : bh, Ml[r][j]);
-                Mh[r][j] = __builtin_fmaf(bp ? Uh[r][k] : Ul[r][k], up ? bh : bl, Mh[r][j]);
+                Ml[r][j] = __builtin_fmaf(bp ? Ul[r][k] : Uh[r][k], tile[ol[r] + k * LD + j], Ml[r][j]);
+                Mh[r][j] = __builtin_fmaf(bp ? Uh[r][k] : Ul[r][k], tile[oh[r] + k * LD + j], Mh[r][j]);
             }
         }
+    }
+    } else {
+#pragma unroll
+        for (int k = 0; k < B; ++k)
+#pragma unroll
+            for (int j = 0; j < B; ++j) {
+                const float bl = tile[k * LD + j], bh = tile2[k * LD + j];
+                const bool bp = bl >= 0.0f;
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const bool up = Ul[r][k] >= 0.0f;
+                    Ml[r][j] = __builtin_fmaf(bp ? Ul[r][k] : Uh[r][k], up ? bl : bh, Ml[r][j]);
+                    Mh[r][j] = __builtin_fmaf(bp ? Uh[r][k] : Ul[r][k], up ? bh : bl, Mh[r][j]);
+                }
+            }
+    }
     __syncthreads();
     stamp(4);
     idct2d_rows_layout_iv<B>(Ml, Mh, tile, tile2, q);  // :204
@@ -547,8 +565,10 @@ template <int B, bool LIST = false>
 __global__ __launch_bounds__(64, kEmbedWaves<B>) void embed_kernel(EmbedArgs a)
 {
     constexpr int L = Geo<B>::L, BPW = Geo<B>::BPW, TS = kEmbedTS<B>;
-    __shared__ __attribute__((aligned(16))) float lds[BPW * TS];        // also svd3's scratch during the SVD
-    __shared__ __attribute__((aligned(16))) float lds2[kLds2Floats<B>];  // source bytes, then the upper-end tiles
+    // the transpose tiles (also svd3's scratch during the SVD), then the source bytes / the
+    // upper-end tiles, in one array (the reconstruction picks a tile by an offset)
+    __shared__ __attribute__((aligned(16))) float lds_all[BPW * TS + kLds2Floats<B>];
+    float *lds = lds_all, *lds2 = lds_all + BPW * TS;
     if constexpr (LIST) {
         // grid-stride over the slow list's segments (their lengths are known on the device only)
         const uint32_t per_frame = (uint32_t)a.nbh * (uint32_t)a.nbw, rows = (uint32_t)a.nframes * (uint32_t)a.nbh;
