@@ -29,7 +29,8 @@
  *     device's end-point selection is exact unless a rank has both on the two sides of the
  *     product, and this block-level test covers that (exact zeros of structured blocks);
  *   keep_k = f32(sigma_k) != 0, g_k = min(sigma_k, min_{j != k} |sigma_k - sigma_j|),
- *   E_k = t / g_k (keep_k; t = 2^-45 s1), Es = t;
+ *   E_k = f32(t / g_k) (keep_k; t = 2^-45 s1; in [2^-45, 2^-25] when the conditioning test
+ *         passes: held as a float on the device), Es = t;
  *   S_k in [f32(max(sigma_k - Es, 0)), f32(sigma_k + Es)]; S'_0 ends f32(f64(end) + c);
  *   keep_k:  U_rk in [f32(u - E_k), f32(u + E_k)], V_jk likewise, B_kj = S'_k x V_jk
  *            (S' >= 0: lo = S'lo v_lo if v_lo >= 0 else S'hi v_lo; hi = S'lo v_hi if
@@ -309,7 +310,7 @@ extern "C" int orc_cert_block(const float *D, const double *U, const double *sig
                 const double d = fabs(sig[k] - sig[j]);
                 g = d < g ? d : g;
             }
-        const double E = t / g;
+        const double E = (double)(float)(t / g);
         for (int r = 0; r < b; ++r) {
             const double u = U[r * b + k];
             Ui[r][k] = {(float)(u - E), (float)(u + E)};

@@ -223,12 +223,12 @@ TMF_DEVI void luma_rows(const uint32_t (&words)[Geo<B>::R][Geo<B>::NW], float (&
 // ---------------------------------------------------------------------------
 // Embed: watermarking.py:163-216 fused, one launch per batch.
 // ---------------------------------------------------------------------------
-// Waves per SIMD the register allocation must allow (1 = unconstrained: the compiler
-// then fits b <= 10 and 14 into 2-3 waves, but b = 12 and 16 overflow into AGPRs and run
-// one wave per SIMD).  Forcing 2 for b = 12 / 16 costs 156 / 256 B of scratch per lane
-// and is faster: embed<12> 283 -> 201 us, embed<16> 531 -> 345 us per 4K frame.
+// Waves per SIMD the register allocation must allow (1 = unconstrained: with the byte
+// certificate's second end points the compiler overflows into AGPRs at b >= 8 and runs one
+// wave per SIMD).  Forcing 2 is faster even where it costs scratch (round 4, before the
+// certificate: embed<12> 283 -> 201 us, embed<16> 531 -> 345 us per 4K frame).
 template <int B>
-constexpr int kEmbedWaves = (B == 8 || B == 10 || B == 12 || B == 16) ? 2 : 1;
+constexpr int kEmbedWaves = (B == 8 || B == 10 || B == 12 || B == 14 || B == 16) ? 2 : 1;
 
 // Strip pass: once at most kDeferMax blocks of a wave still need f64 sweeps after a sweep
 // and its Newton try, the wave leaves them to the list pass instead of running another
@@ -272,6 +272,13 @@ constexpr int kLds2Floats = kPixWords<B> > Geo<B>::BPW * kHiTile<B> ? kPixWords<
 // (the other sizes, where the offset form costs registers)
 template <int B>
 constexpr bool kOffsetPick = B == 8 || B == 16;
+
+// b = 10 / 14 keep the reconstruction's fma chains in their (k-outer) source order: left free,
+// the compiler regroups them per output element and spills every element of Bm it reads
+// ahead of its use (272 / 282 VGPRs spilled -> 0 / 5; embed<14> 613 -> 360 us per 4K frame,
+// embed<10> 271 -> 247).  At b = 8 / 16 the free schedule is faster (128 vs 139 us, 334 vs 364).
+template <int B>
+constexpr bool kPinChain = B == 10 || B == 14;
 
 // One wave's blocks: strip mode (LIST = false: the strip of blockIdx) or list mode (pos and
 // id from the slow list).  id = (frame * nbh + bi) * nbw + bj, relative to a.src.
@@ -361,13 +368,10 @@ TMF_DEVI void embed_blocks(const EmbedArgs &a, const StripPos &pos, uint32_t id,
     // flagged and deferred blocks keep point intervals: the point path's values)
     const bool cert = !zero && !flat && !flag20 && !slow;
     const double tE = cert ? kCertScale * s1 : 0.0;
-    double E[B];
-    bool keep[B];
+    // E_k = f32(tE / g_k): in [2^-45, 2^-25] for a certified block (g_k >= 2^-20 s1), held as a float
+    float E[B];
 #pragma unroll
-    for (int k = 0; k < B; ++k) {
-        keep[k] = zero || (float)sig[k] != 0.0f;
-        E[k] = cert && keep[k] ? tE / gk[k] : 0.0;
-    }
+    for (int k = 0; k < B; ++k) E[k] = cert && (float)sig[k] != 0.0f ? (float)(tE / gk[k]) : 0.0f;
     // Sort descending (oracle: odd-even transposition sort, stable) as ranks: k goes to
     // position rk[k] = #{j < k: sig[j] >= sig[k]} + #{j > k: sig[j] > sig[k]}.  The
     // permutation is applied through LDS: U's columns here, Vt's rows with the B store.
@@ -382,23 +386,6 @@ TMF_DEVI void embed_blocks(const EmbedArgs &a, const StripPos &pos, uint32_t id,
             rk[k] += ge;
             rk[j] += 1 - ge;
         }
-    // N7 blend (:198): S[0] = f32(f64(S[0]) + alpha * (w / 255.0)), S[0] the largest; as
-    // intervals [f32(max(sigma - Es, 0)), f32(sigma + Es)] blended at both ends
-    const uint32_t wv = pos.valid ? a.wm[(int64_t)pos.bi * a.nbw + pos.bj] : 0u;
-    const double cw = a.alpha * ((double)wv / 255.0);
-    float Sl[B], Sh[B];
-    bool neg = false;  // alpha < 0 pushing S'[0] below zero: outside the certificate's S' >= 0
-#pragma unroll
-    for (int k = 0; k < B; ++k) {
-        const double lo = sig[k] - tE;
-        Sl[k] = (float)(lo > 0.0 ? lo : 0.0);
-        Sh[k] = (float)(sig[k] + tE);
-        if (rk[k] == 0) {
-            Sl[k] = (float)((double)Sl[k] + cw);
-            Sh[k] = (float)((double)Sh[k] + cw);
-            neg = !(Sl[k] >= 0.0f);
-        }
-    }
     // U = A / sigma as f32 intervals [f32(u - E), f32(u + E)]; triplets that do not reach the
     // output (f32(sigma) == 0) take U = [2, 2] against B = [-2 S', 2 S'] (|f32 entries| <= 1)
     // over this lane's rows of the triplets that reach the output: an interval that contains 0,
@@ -412,12 +399,12 @@ TMF_DEVI void embed_blocks(const EmbedArgs &a, const StripPos &pos, uint32_t id,
             float ul, uh;
             if (zero) {
                 ul = uh = (q * R + r == k) ? 1.0f : 0.0f;
-            } else if (!keep[k]) {
+            } else if ((float)sig[k] == 0.0f) {  // the triplet does not reach the output
                 ul = uh = 2.0f;
             } else {
                 const double u = A[r][k] * inv;
-                ul = (float)(u - E[k]);
-                uh = (float)(u + E[k]);
+                ul = (float)(u - (double)E[k]);
+                uh = (float)(u + (double)E[k]);
             }
 
             if (real_row<B>(q, r)) {
@@ -439,6 +426,23 @@ TMF_DEVI void embed_blocks(const EmbedArgs &a, const StripPos &pos, uint32_t id,
         }
     __syncthreads();
 
+    // N7 blend (:198): S[0] = f32(f64(S[0]) + alpha * (w / 255.0)), S[0] the largest; as
+    // intervals [f32(max(sigma - Es, 0)), f32(sigma + Es)] blended at both ends
+    const uint32_t wv = pos.valid ? a.wm[(int64_t)pos.bi * a.nbw + pos.bj] : 0u;
+    const double cw = a.alpha * ((double)wv / 255.0);
+    float Sl[B], Sh[B];
+    bool neg = false;  // alpha < 0 pushing S'[0] below zero: outside the certificate's S' >= 0
+#pragma unroll
+    for (int k = 0; k < B; ++k) {
+        const double lo = sig[k] - tE;
+        Sl[k] = (float)(lo > 0.0 ? lo : 0.0);
+        Sh[k] = (float)(sig[k] + tE);
+        if (rk[k] == 0) {
+            Sl[k] = (float)((double)Sl[k] + cw);
+            Sh[k] = (float)((double)Sh[k] + cw);
+            neg = !(Sl[k] >= 0.0f);
+        }
+    }
     // N8 (:201): Bm[t][j] = S'[t] * Vt[t][j] (this lane's rows j of V, row t = rank), then M = U @ Bm,
     // both ends (S' >= 0: the lower end is S'lo v if v >= 0, else S'hi v; the upper alike)
 #pragma unroll
@@ -448,16 +452,16 @@ TMF_DEVI void embed_blocks(const EmbedArgs &a, const StripPos &pos, uint32_t id,
             float bl, bh;
             if (zero) {
                 bl = bh = Sl[k] * ((q * R + r == k) ? 1.0f : 0.0f);
-            } else if (!keep[k]) {
+            } else if ((float)sig[k] == 0.0f) {
                 bl = -2.0f * Sh[k];
                 bh = 2.0f * Sh[k];
             } else {
-                const float vl = (float)(V[r][k] - E[k]), vh = (float)(V[r][k] + E[k]);
+                const float vl = (float)(V[r][k] - (double)E[k]), vh = (float)(V[r][k] + (double)E[k]);
                 bl = vl >= 0.0f ? Sl[k] * vl : Sh[k] * vl;
                 bh = vh <= 0.0f ? Sl[k] * vh : Sh[k] * vh;
             }
             if (real_row<B>(q, r)) {
-                str |= (int)keep[k] & (int)(bl < 0.0f) & (int)(bh > 0.0f);
+                str |= (int)(zero || (float)sig[k] != 0.0f) & (int)(bl < 0.0f) & (int)(bh > 0.0f);
                 wid |= (int)(bl != bh);
                 tile[rk[k] * LD + q * R + r] = bl;
                 tile2[rk[k] * LD + q * R + r] = bh;
@@ -501,6 +505,7 @@ TMF_DEVI void embed_blocks(const EmbedArgs &a, const StripPos &pos, uint32_t id,
             for (int r = 0; r < R; ++r) {
                 Ml[r][j] = __builtin_fmaf(bp ? Ul[r][k] : Uh[r][k], tile[ol[r] + k * LD + j], Ml[r][j]);
                 Mh[r][j] = __builtin_fmaf(bp ? Uh[r][k] : Ul[r][k], tile[oh[r] + k * LD + j], Mh[r][j]);
+                if constexpr (kPinChain<B>) pin_order(Ml[r][j], Mh[r][j]);
             }
         }
     }
@@ -509,6 +514,7 @@ TMF_DEVI void embed_blocks(const EmbedArgs &a, const StripPos &pos, uint32_t id,
         for (int k = 0; k < B; ++k)
 #pragma unroll
             for (int j = 0; j < B; ++j) {
+                lds_order();  // one element of Bm at a time (hoisting them spills at b = 10..14)
                 const float bl = tile[k * LD + j], bh = tile2[k * LD + j];
                 const bool bp = bl >= 0.0f;
 #pragma unroll
@@ -516,6 +522,7 @@ TMF_DEVI void embed_blocks(const EmbedArgs &a, const StripPos &pos, uint32_t id,
                     const bool up = Ul[r][k] >= 0.0f;
                     Ml[r][j] = __builtin_fmaf(bp ? Ul[r][k] : Uh[r][k], up ? bl : bh, Ml[r][j]);
                     Mh[r][j] = __builtin_fmaf(bp ? Uh[r][k] : Ul[r][k], up ? bh : bl, Mh[r][j]);
+                    if constexpr (kPinChain<B>) pin_order(Ml[r][j], Mh[r][j]);
                 }
             }
     }

@@ -959,6 +959,8 @@ constexpr uint32_t sched_nibbles()
 // keeps the compiler from moving this block's LDS norm accesses across a round boundary
 // (the lanes of a wave see each other's LDS writes in program order)
 TMF_DEVI void lds_order() { asm volatile("" ::: "memory"); }
+// the values leave this point in order: the arithmetic producing them is not moved past it
+TMF_DEVI void pin_order(float &a, float &b) { asm volatile("" : "+v"(a), "+v"(b)); }
 
 // One sweep (oracle jacobi_sweep() / the loop body of jacobi()): nrm are recomputed, the
 // b-1 rounds of b/2 disjoint pairs rotate every pair that passes the tests.  `enable`
