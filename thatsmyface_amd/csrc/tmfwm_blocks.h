@@ -250,7 +250,17 @@ constexpr bool kParkD = B == 16;
 template <int B>
 constexpr int kEmbedTS0 = B * (B + 1) > kScratchFloats<B, Geo<B>::L> ? B * (B + 1) : kScratchFloats<B, Geo<B>::L>;
 template <int B>
-constexpr int kEmbedTS = ((kParkD<B> && kParkOff<Geo<B>::L> + B * B > kEmbedTS0<B> ? kParkOff<Geo<B>::L> + B * B : kEmbedTS0<B>) + 1) & ~1;
+constexpr int kEmbedTS1 = ((kParkD<B> && kParkOff<Geo<B>::L> + B * B > kEmbedTS0<B> ? kParkOff<Geo<B>::L> + B * B : kEmbedTS0<B>) + 1) & ~1;
+// Bank spreading for the reconstruction's LDS reads (ds_read_b32: bank = dword address mod 32
+// over each 32-lane half): at b = 8 a half holds 16 blocks, at b = 16 four, and each lane reads
+// its block's lower-end or upper-end tile.  Tile strides 73 (b = 8: 9 g mod 32, distinct over
+// 16 blocks) and 312 (b = 16: 24 g) in both regions, with the upper-end region kHiPad dwords
+// further on (16 / 4), put every (block, end) of a half on a bank of its own; with strides 72
+// and 72 (b = 16: 312 and 272) four (two) of them shared one, and bank conflicts were 75 % of
+// embed<8>'s LDS cycles (profiles/r05/r05h).
+template <int B>
+constexpr int kEmbedTS = B == 8 ? 73 : kEmbedTS1<B>;
+static_assert(kEmbedTS<8> >= kEmbedTS1<8> && kEmbedTS<16> % 32 == 24, "tile strides");
 
 // Byte certificate of the hybrid route (oracle tmfwm_cert.cpp): LAPACK's f64
 // factors lie within E_k = kCertScale s1 / g_k of the Jacobi route's, every singular value
@@ -264,7 +274,9 @@ constexpr double kCertScale = 0x1p-45;
 template <int B>
 constexpr int kPixWords = Geo<B>::R * Geo<B>::NW * 64;
 template <int B>
-constexpr int kHiTile = B * (B + 1);
+constexpr int kHiTile = B == 8 || B == 16 ? kEmbedTS<B> : B * (B + 1);
+template <int B>
+constexpr int kHiPad = B == 8 ? 16 : B == 16 ? 4 : 0;
 template <int B>
 constexpr int kLds2Floats = kPixWords<B> > Geo<B>::BPW * kHiTile<B> ? kPixWords<B> : Geo<B>::BPW * kHiTile<B>;
 
@@ -396,16 +408,13 @@ TMF_DEVI void embed_blocks(const EmbedArgs &a, const StripPos &pos, uint32_t id,
         const double inv = 1.0 / sig[k];
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            float ul, uh;
-            if (zero) {
-                ul = uh = (q * R + r == k) ? 1.0f : 0.0f;
-            } else if ((float)sig[k] == 0.0f) {  // the triplet does not reach the output
-                ul = uh = 2.0f;
-            } else {
-                const double u = A[r][k] * inv;
-                ul = (float)(u - (double)E[k]);
-                uh = (float)(u + (double)E[k]);
-            }
+            // branch-free (selects): the three cases are lane-divergent
+            const double u = A[r][k] * inv;
+            float ul = (float)(u - (double)E[k]), uh = (float)(u + (double)E[k]);
+            const float id = (q * R + r == k) ? 1.0f : 0.0f;
+            const bool out = (float)sig[k] != 0.0f;  // the triplet reaches the output
+            ul = zero ? id : out ? ul : 2.0f;
+            uh = zero ? id : out ? uh : 2.0f;
 
             if (real_row<B>(q, r)) {
                 tile[(q * R + r) * LD + rk[k]] = ul;
@@ -437,11 +446,11 @@ TMF_DEVI void embed_blocks(const EmbedArgs &a, const StripPos &pos, uint32_t id,
         const double lo = sig[k] - tE;
         Sl[k] = (float)(lo > 0.0 ? lo : 0.0);
         Sh[k] = (float)(sig[k] + tE);
-        if (rk[k] == 0) {
-            Sl[k] = (float)((double)Sl[k] + cw);
-            Sh[k] = (float)((double)Sh[k] + cw);
-            neg = !(Sl[k] >= 0.0f);
-        }
+        const bool top = rk[k] == 0;
+        const float bl0 = (float)((double)Sl[k] + cw), bh0 = (float)((double)Sh[k] + cw);
+        Sl[k] = top ? bl0 : Sl[k];
+        Sh[k] = top ? bh0 : Sh[k];
+        neg = neg || (top && !(bl0 >= 0.0f));
     }
     // N8 (:201): Bm[t][j] = S'[t] * Vt[t][j] (this lane's rows j of V, row t = rank), then M = U @ Bm,
     // both ends (S' >= 0: the lower end is S'lo v if v >= 0, else S'hi v; the upper alike)
@@ -449,17 +458,13 @@ TMF_DEVI void embed_blocks(const EmbedArgs &a, const StripPos &pos, uint32_t id,
     for (int k = 0; k < B; ++k) {
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            float bl, bh;
-            if (zero) {
-                bl = bh = Sl[k] * ((q * R + r == k) ? 1.0f : 0.0f);
-            } else if ((float)sig[k] == 0.0f) {
-                bl = -2.0f * Sh[k];
-                bh = 2.0f * Sh[k];
-            } else {
-                const float vl = (float)(V[r][k] - (double)E[k]), vh = (float)(V[r][k] + (double)E[k]);
-                bl = vl >= 0.0f ? Sl[k] * vl : Sh[k] * vl;
-                bh = vh <= 0.0f ? Sl[k] * vh : Sh[k] * vh;
-            }
+            const float vl = (float)(V[r][k] - (double)E[k]), vh = (float)(V[r][k] + (double)E[k]);
+            float bl = vl >= 0.0f ? Sl[k] * vl : Sh[k] * vl;
+            float bh = vh <= 0.0f ? Sl[k] * vh : Sh[k] * vh;
+            const float bid = Sl[k] * ((q * R + r == k) ? 1.0f : 0.0f);
+            const bool out = (float)sig[k] != 0.0f;
+            bl = zero ? bid : out ? bl : -2.0f * Sh[k];
+            bh = zero ? bid : out ? bh : 2.0f * Sh[k];
             if (real_row<B>(q, r)) {
                 str |= (int)(zero || (float)sig[k] != 0.0f) & (int)(bl < 0.0f) & (int)(bh > 0.0f);
                 wid |= (int)(bl != bh);
@@ -546,8 +551,15 @@ TMF_DEVI void embed_blocks(const EmbedArgs &a, const StripPos &pos, uint32_t id,
                 const uint32_t R0 = byte_at(words[r], 3 * c), G0 = byte_at(words[r], 3 * c + 1), B0 = byte_at(words[r], 3 * c + 2);
                 chroma(R0, G0, B0, cbs, crs);
                 uint32_t R8, G8, B8;
-                colour_inv(Ml[r][c], cbs, crs, R8, G8, B8);
-                const bool wide = Ml[r][c] != Mh[r][c];
+                float fr;
+                colour_inv_frac(Ml[r][c], cbs, crs, R8, G8, B8, fr);
+                // Every channel is monotone in Y, and from Y's lower end to its upper end each
+                // scaled value p = f32(clip(v) * 255) grows by at most 255 dY + 255 * 2^-24 +
+                // 2^-16 (v's f32 rounding on [0, 1], then p's) < 255.1 dY + 2^-14, dY = f32(Yh -
+                // Yl); so the bytes cannot differ unless frac(p) + that reaches 1, and only then
+                // are the upper end's bytes computed
+                const float dy = Mh[r][c] - Ml[r][c];
+                const bool wide = dy != 0.0f && fr + __builtin_fmaf(dy, 255.1f, 0x1p-14f) >= 1.0f;
                 if (__builtin_amdgcn_ballot_w64(wide) != 0 && wide) {
                     uint32_t R9, G9, B9;
                     colour_inv(Mh[r][c], cbs, crs, R9, G9, B9);
@@ -574,8 +586,8 @@ __global__ __launch_bounds__(64, kEmbedWaves<B>) void embed_kernel(EmbedArgs a)
     constexpr int L = Geo<B>::L, BPW = Geo<B>::BPW, TS = kEmbedTS<B>;
     // the transpose tiles (also svd3's scratch during the SVD), then the source bytes / the
     // upper-end tiles, in one array (the reconstruction picks a tile by an offset)
-    __shared__ __attribute__((aligned(16))) float lds_all[BPW * TS + kLds2Floats<B>];
-    float *lds = lds_all, *lds2 = lds_all + BPW * TS;
+    __shared__ __attribute__((aligned(16))) float lds_all[BPW * TS + kHiPad<B> + kLds2Floats<B>];
+    float *lds = lds_all, *lds2 = lds_all + BPW * TS + kHiPad<B>;
     if constexpr (LIST) {
         // grid-stride over the slow list's segments (their lengths are known on the device only)
         const uint32_t per_frame = (uint32_t)a.nbh * (uint32_t)a.nbw, rows = (uint32_t)a.nframes * (uint32_t)a.nbh;

@@ -73,6 +73,21 @@ TMF_DEVI void colour_inv(float y, float cbs, float crs, uint32_t &R, uint32_t &G
     B = u8_from_unit((float)(Y + 1.773 * CB));
 }
 
+// colour_inv that also returns the largest fractional part of the three scaled channel
+// values p = f32(clip(v) * 255) whose truncation gives the bytes: the byte certificate's
+// test of a Y interval (blocks.h embed_blocks)
+TMF_DEVI void colour_inv_frac(float y, float cbs, float crs, uint32_t &R, uint32_t &G, uint32_t &B, float &fr)
+{
+    const double Y = y, CB = cbs - 0.5f, CR = crs - 0.5f;
+    const float pr = __builtin_amdgcn_fmed3f((float)__builtin_fma(1.403, CR, Y), 0.0f, 1.0f) * 255.0f;
+    const float pg = __builtin_amdgcn_fmed3f((float)__builtin_fma(-0.714, CR, Y + -0.344 * CB), 0.0f, 1.0f) * 255.0f;
+    const float pb = __builtin_amdgcn_fmed3f((float)(Y + 1.773 * CB), 0.0f, 1.0f) * 255.0f;
+    R = (uint32_t)pr;
+    G = (uint32_t)pg;
+    B = (uint32_t)pb;
+    fr = __builtin_fmaxf(__builtin_amdgcn_fractf(pr), __builtin_fmaxf(__builtin_amdgcn_fractf(pg), __builtin_amdgcn_fractf(pb)));
+}
+
 // ---------------------------------------------------------------------------
 // The module-level helpers on non-uint8 inputs (the frame kernels above only ever
 // see uint8 pixels).  rgb_to_ycbcr casts any numeric array with np.array(img,
