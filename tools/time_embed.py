@@ -24,6 +24,7 @@ def main():
     p.add_argument("--reps", type=int, default=3)
     p.add_argument("--kind", choices=["noise", "photo"], default="noise", help="covers: the bench's noise or camera-like")
     p.add_argument("--wm", choices=["noise", "qr"], default="noise", help="watermark tile: uniform bytes or binary (QR)")
+    p.add_argument("--route", choices=["hybrid", "reference"], default="hybrid")
     a = p.parse_args()
     dev = torch.device("cuda", 0)
     b = a.block
@@ -33,12 +34,13 @@ def main():
     fr = photo_covers(a.frames, 2160, 3840, 5, dev) if a.kind == "photo" else batch.synth_frames(a.frames, 2160, 3840, device=dev)
     tile = qr_tile(2160 // b, 3840 // b, 1, dev) if a.wm == "qr" else batch.synth_tile(2160 // b, 3840 // b, device=dev)
     st = {}
-    out = batch.embed_batch(fr, tile, b, 0.1, stats=st)
-    ext = batch.extract_batch(out, fr, b, 0.1)
+    rt = a.route
+    out = batch.embed_batch(fr, tile, b, 0.1, stats=st, route=rt)
+    ext = batch.extract_batch(out, fr, b, 0.1, route=rt)
     torch.cuda.synchronize()
     res = {}
-    for name, fn in (("embed", lambda: batch.embed_batch(fr, tile, b, 0.1, out=out)),
-                     ("extract", lambda: batch.extract_batch(out, fr, b, 0.1, out=ext))):
+    for name, fn in (("embed", lambda: batch.embed_batch(fr, tile, b, 0.1, out=out, route=rt)),
+                     ("extract", lambda: batch.extract_batch(out, fr, b, 0.1, out=ext, route=rt))):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(a.reps):
@@ -47,7 +49,7 @@ def main():
         torch.cuda.synchronize()
         res[name] = round(e0.elapsed_time(e1) * 1000 / a.reps / a.frames, 2)
     print(json.dumps({"lib": os.path.basename(os.environ.get("TMFWM_LIB", "libtmfwm.so")), "block": b, "kind": a.kind, "wm": a.wm,
-                      "frames": a.frames, "dgesdd_route_blocks": st.get("lapack_blocks"), "us_per_frame": res}))
+                      "route": rt, "frames": a.frames, "dgesdd_route_blocks": st.get("lapack_blocks"), "us_per_frame": res}))
 
 
 if __name__ == "__main__":
