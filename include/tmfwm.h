@@ -113,8 +113,9 @@ int tmfwm_embed_ex(const uint8_t *rgb, int64_t n_frames, int32_t height, int32_t
  * tmfwm_embed_ex with an explicit SVD route (ABI 7): TMFWM_ROUTE_HYBRID is tmfwm_embed_ex;
  * TMFWM_ROUTE_REFERENCE sends every block through the dgesdd route (LAPACK dgesdd + the
  * OpenBLAS kernels numpy calls, restated operation by operation), so each output byte is
- * computed by the reference's own arithmetic rather than agreeing with it up to the
- * hybrid route's measured rounding-coincidence rate.  About two orders of magnitude less
+ * computed by the reference's own arithmetic, with no certificate and no error bound to rely
+ * on (the hybrid route's bytes equal it through its byte certificate, which rests on one
+ * measured bound).  About two orders of magnitude less
  * throughput than the hybrid route; *n_lapack_blocks then counts every block.
  */
 int tmfwm_embed_route(const uint8_t *rgb, int64_t n_frames, int32_t height, int32_t width, int64_t frame_stride,
