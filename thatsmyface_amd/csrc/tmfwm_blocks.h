@@ -285,6 +285,13 @@ constexpr int kLds2Floats = kPixWords<B> > Geo<B>::BPW * kHiTile<B> ? kPixWords<
 template <int B>
 constexpr bool kOffsetPick = B == 8 || B == 16;
 
+// b = 16 reads its source bytes again from global memory (L2) for the colour phase instead of
+// parking them in LDS and carrying them through the certificate in registers: spilled VGPRs
+// 27 -> 8, embed<16> -1 % per 4K frame; at b = 8 it is slower (+1.5 % on noise covers,
+// profiles/r05/r05q_ab.log)
+template <int B>
+constexpr bool kReloadBytes = B == 16;
+
 // b = 10 / 14 keep the reconstruction's fma chains in their (k-outer) source order: left free,
 // the compiler regroups them per output element and spills every element of Bm it reads
 // ahead of its use (272 / 282 VGPRs spilled -> 0 / 5; embed<14> 613 -> 360 us per 4K frame,
@@ -312,10 +319,12 @@ TMF_DEVI void embed_blocks(const EmbedArgs &a, const StripPos &pos, uint32_t id,
         uint32_t words[R][NW];
         load_block_rows<B>(src, a.W, pos, q, a.aligned, words);
         luma_rows<B>(words, x);
+        if constexpr (!kReloadBytes<B>) {
 #pragma unroll
-        for (int r = 0; r < R; ++r)
+            for (int r = 0; r < R; ++r)
 #pragma unroll
-            for (int i = 0; i < NW; ++i) pix[r * NW + i][lane] = words[r][i];
+                for (int i = 0; i < NW; ++i) pix[r * NW + i][lane] = words[r][i];
+        }
     }
     dct2d_rows_layout<B, false>(x, tile, q);  // :192
     stamp(0);
@@ -338,12 +347,15 @@ TMF_DEVI void embed_blocks(const EmbedArgs &a, const StripPos &pos, uint32_t id,
         a.slow_list[shard_base(s, (uint32_t)a.nframes * (uint32_t)a.nbh, (uint32_t)a.nbw) +
                     atomicAdd(a.slow_shards + s * kShardStride, 1u)] = id;
     }
-    // this lane's source bytes back to registers: their LDS becomes the upper-end tiles
+    // this lane's source bytes back to registers (b = 16: from global memory at the colour
+    // phase instead): their LDS becomes the upper-end tiles
     uint32_t words[R][NW];
+    if constexpr (!kReloadBytes<B>) {
 #pragma unroll
-    for (int r = 0; r < R; ++r)
+        for (int r = 0; r < R; ++r)
 #pragma unroll
-        for (int i = 0; i < NW; ++i) words[r][i] = pix[r * NW + i][lane];
+            for (int i = 0; i < NW; ++i) words[r][i] = pix[r * NW + i][lane];
+    }
     __syncthreads();
 
     // singular values (oracle orc_svd_block: sigma_k = |a_k|, u_k = a_k / sigma_k)
@@ -540,6 +552,7 @@ TMF_DEVI void embed_blocks(const EmbedArgs &a, const StripPos &pos, uint32_t id,
     // bytes; a pixel whose ends give other bytes leaves the block undecided
     bool unc = neg;
     if (pos.valid && !slow) {
+        if constexpr (kReloadBytes<B>) load_block_rows<B>(src, a.W, pos, q, a.aligned, words);
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             uint32_t out[Geo<B>::NW];
