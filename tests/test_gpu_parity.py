@@ -886,6 +886,29 @@ def test_hybrid_vs_reference_route_4k(dev, b, wm):
     assert nb == 0 and torch.equal(oh, orf), nb
 
 
+@pytest.mark.parametrize("b", [8, 12, 16])
+def test_hybrid_vs_reference_route_alpha_edges(dev, b):
+    """The certificate's edges of the blend (watermarking.py:198): alpha = 0 (S' = S), large
+    alpha (up to the slider's golden 1.0) and a negative alpha that pushes S'[0] below zero
+    (outside the certificate's sign rule: those blocks take the dgesdd route) -- the hybrid
+    route's bytes equal the reference route's on camera-like covers with a QR watermark."""
+    import sys as _sys
+
+    _sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "exp"))
+    from route_diff_gpu import photo_covers
+
+    from thatsmyface_amd import batch
+
+    H, W, n = 544, 960, 4
+    fr = photo_covers(n, H, W, 300 + b, dev)
+    tile = torch.from_numpy(_u8(301 + b, (H // b, W // b)) & np.uint8(1)).to(dev) * 255
+    for alpha in (0.0, 0.5, 1.0, -0.05, -5.0):
+        st = {}
+        oh = batch.embed_batch(fr, tile, b, alpha, route="hybrid", stats=st)
+        orf = batch.embed_batch(fr, tile, b, alpha, route="reference")
+        assert torch.equal(oh, orf), (b, alpha, st)
+
+
 @pytest.mark.parametrize("mem", ["host", "device"])
 def test_pixel_layouts_px_entry_points(dev, mem):
     """tmfwm_embed_px / tmfwm_extract_px (ABI 8): 4-byte (PIL RGBX) and 3-byte frames in any
