@@ -88,3 +88,18 @@ def test_noise_covers_decided():
     st = {}
     O.embed_frame(cov, tile, b, 0.1, route="hybrid", stats=st)
     assert st["fallback_blocks"] <= 0.001 * (H // b) * (W // b) + 1, st
+
+
+def test_device_and_oracle_share_the_bound():
+    """The device certificate (tmfwm_blocks.h) and its oracle restatement (tmfwm_cert.cpp) use the
+    same K (kCertScale = K 2^-53 = 2^-45) and hold E_k as f32(tE / g_k) on both sides."""
+    import os
+    import re
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    dev = open(os.path.join(root, "thatsmyface_amd", "csrc", "tmfwm_blocks.h")).read()
+    orc = open(os.path.join(root, "oracle", "tmfwm_cert.cpp")).read()
+    rx = re.compile(r"kCertScale\s*=\s*([0-9a-fx.p+-]+)")
+    assert rx.search(dev).group(1) == rx.search(orc).group(1) == "0x1p-45"
+    assert "(float)(tE / gk[k])" in dev
+    assert re.search(r"\(double\)\(float\)\(t / g\)", orc)
