@@ -39,9 +39,11 @@ template <int B, int ITERS>
 TMF_DEVI void extract_sigmas(const ExtractArgs &a, const StripPos &pos, float *tile, int q, float &sw, float &so, bool &ok)
 {
     constexpr int R = Geo<B>::R, L = Geo<B>::L;
-    if constexpr (B <= 12) {
+    if constexpr (B <= 14) {
         // both images' rows requested up front (one exposed HBM latency per wave, not two),
-        // and both power iterations interleaved (sigma1_certified, NI = 2)
+        // and both power iterations interleaved (sigma1_certified, NI = 2); at b = 16 the
+        // interleaved form measured the same as the sequential one, at b = 14 -3 %
+        // (profiles/r05/r05y_ab.log)
         float x[2][R][B];
         {
             uint32_t ww[R][Geo<B>::NW], wo[R][Geo<B>::NW];
