@@ -1,6 +1,7 @@
 """Host-side logic of the drop-in module (no GPU): settings resolution
 (watermarking.py:10-20), watermark resize (:86-132) against the reference's
 tiles, and the argument checks that run before any kernel."""
+import gc
 import io
 import sys
 import types
@@ -100,6 +101,46 @@ def test_zero_copy_pil_helpers():
     del out, buf  # the pool counts every reference, this test's own included
     gc.collect()
     assert W._take_out(48 * 80 * 4).ctypes.data == where
+
+
+def test_pool_finalizer_runs_under_the_pool_lock():
+    """an output image in a reference cycle is finalized by whichever thread triggers
+    the cyclic GC -- possibly one that holds _pool_lock (in _take_out).  The finalizer must not
+    take the lock (a plain Lock would deadlock the thread on itself)."""
+    import threading
+
+    if W._arrow() is None:
+        pytest.skip("zero-copy path unavailable (pyarrow / Pillow Arrow interface)")
+    buf = W._take_out(16 * 16 * 4)
+    img = W._rgb_from_rgbx(buf, 16, 16)
+    cyc = [img]
+    cyc.append(cyc)  # collectable only by the cyclic GC
+    del img, cyc, buf
+    done = threading.Event()
+
+    def run():
+        with W._pool_lock:
+            gc.collect()  # the image's finalizer runs here, inside the locked region
+        done.set()
+
+    t = threading.Thread(target=run, daemon=True)
+    t.start()
+    assert done.wait(10), "finalizer deadlocked on _pool_lock"
+    assert W._take_out(16 * 16 * 4) is not None
+
+
+def test_pool_buffer_returned_after_failed_call(monkeypatch):
+    """a pooled buffer whose C call raised (no image built) is free again."""
+    if W._arrow() is None:
+        pytest.skip("zero-copy path unavailable (pyarrow / Pillow Arrow interface)")
+    n = 24 * 40 * 4
+    W._out_pool.pop(n, None)
+    buf = W._take_out(n)
+    where = buf.ctypes.data
+    W._give_back(buf)
+    del buf
+    gc.collect()
+    assert W._take_out(n).ctypes.data == where
 
 
 def test_zero_copy_needs_pillow_arrow(monkeypatch):

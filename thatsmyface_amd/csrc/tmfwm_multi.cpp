@@ -176,34 +176,42 @@ struct BufCache {
         sizes[p] = bytes;
         return p;
     }
+    // hipFree synchronises the device: it runs after the mutex is released, so returning a
+    // buffer never stalls the other shards' lease / give_back behind an idle-wait
     void give_back(int dev, void *p)
     {
         if (!p) return;
-        std::lock_guard<std::mutex> lk(mu);
-        if ((int)free.count(dev) >= kKeep) {  // the oldest cached buffer of the device goes
-            auto it = free.find(dev);
-            (void)hipFree(it->second.second);
-            sizes.erase(it->second.second);
-            free.erase(it);
+        void *evict = nullptr;
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            if ((int)free.count(dev) >= kKeep) {  // the oldest cached buffer of the device goes
+                auto it = free.find(dev);
+                evict = it->second.second;
+                sizes.erase(evict);
+                free.erase(it);
+            }
+            free.emplace(dev, std::make_pair(sizes[p], p));
         }
-        free.emplace(dev, std::make_pair(sizes[p], p));
+        if (evict) (void)hipFree(evict);
     }
     // frees the cached (not leased) buffers of one device, or of every device (dev < 0)
     int release(int dev)
     {
-        std::lock_guard<std::mutex> lk(mu);
-        int n = 0;
-        for (auto it = free.begin(); it != free.end();) {
-            if (dev >= 0 && it->first != dev) {
-                ++it;
-                continue;
+        std::vector<void *> gone;
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            for (auto it = free.begin(); it != free.end();) {
+                if (dev >= 0 && it->first != dev) {
+                    ++it;
+                    continue;
+                }
+                gone.push_back(it->second.second);
+                sizes.erase(it->second.second);
+                it = free.erase(it);
             }
-            (void)hipFree(it->second.second);
-            sizes.erase(it->second.second);
-            it = free.erase(it);
-            ++n;
         }
-        return n;
+        for (void *p : gone) (void)hipFree(p);
+        return (int)gone.size();
     }
 };
 

@@ -241,9 +241,11 @@ def _rgbx_view(image):
 
 
 def _release(buf: np.ndarray) -> None:
-    with _pool_lock:
-        if any(b is buf for b in _out_pool.get(buf.size, ())):  # pooled: free for the next call
-            _out_free.add(id(buf))
+    # Lock-free: a finalizer runs in whichever thread triggers the collection, possibly one that
+    # already holds _pool_lock.  dict.get, iterating a list another thread may append to, and
+    # set.add are each atomic under the GIL; _take_out re-checks pool membership under the lock.
+    if any(b is buf for b in _out_pool.get(buf.size, ())):  # pooled: free for the next call
+        _out_free.add(id(buf))
 
 
 def _take_out(nbytes: int) -> np.ndarray:
@@ -260,8 +262,14 @@ def _take_out(nbytes: int) -> np.ndarray:
                 return b
         b = np.empty(nbytes, np.uint8)
         if len(lst) < _POOL_KEEP:
+            _out_free.discard(id(b))  # a stale id of a collected, unpooled buffer at this address
             lst.append(b)
         return b
+
+
+def _give_back(buf: np.ndarray) -> None:
+    """A buffer from _take_out that no image was built around (the call failed): free again."""
+    _release(buf)
 
 
 def _rgb_from_rgbx(buf: np.ndarray, width: int, height: int):
@@ -311,11 +319,15 @@ def embed_watermark(image, watermark_data, preserve_ratio=False, custom_settings
             src, src_px = _ptr(keep), _lib.PIX_RGB
         out = _take_out(height * width * 4)
         L = _lib.load()
-        _lib.check(
-            L.tmfwm_embed_px(src, src_px, height * width * src_px, 1, height, width, _ptr(tile), block_size, float(alpha),
-                             _ptr(out), _lib.PIX_RGBX, height * width * 4, _lib.MEM_HOST, None, route, None),
-            "embed_watermark",
-        )
+        try:
+            _lib.check(
+                L.tmfwm_embed_px(src, src_px, height * width * src_px, 1, height, width, _ptr(tile), block_size, float(alpha),
+                                 _ptr(out), _lib.PIX_RGBX, height * width * 4, _lib.MEM_HOST, None, route, None),
+                "embed_watermark",
+            )
+        except BaseException:
+            _give_back(out)
+            raise
         del keep
         return _rgb_from_rgbx(out, width, height)
     rgb = np.ascontiguousarray(np.asarray(image, dtype=np.uint8))
