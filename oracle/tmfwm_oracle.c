@@ -960,6 +960,46 @@ static void apply_f(double *X, const float *F, int b)
     }
 }
 
+/* The step's acceptance test (round 6; tests/k_corpus.py).  Besides every
+ * |F_ij| <= 2^-27, the step's neglected second-order terms must stay small on every pair's
+ * own scale: they put a coupling of about sum_i F_ij F_ik G_ii on the pair (j, k), with G_ii up
+ * to sigma_1^2, and the absolute test alone left the small triplets of graded blocks
+ * (sigma_k ~ 1e-5 sigma_1) off by up to 447 units of 2^-53 sigma_1 / g_k.  With x = 2^27 |F|,
+ * r_k = f32(G_kk) * (1 / f32(max G)) and q_j = sum_i x_ij^2 r_i -- an fmaf chain per column in
+ * the sweep's pair order (round s = 0..b-2, each round's pair (i, j) adding x^2 r_j to q_i and
+ * x^2 r_i to q_j) -- the step is taken only if every pair has q_j q_k <= 64 (r_j + r_k): by
+ * Cauchy-Schwarz sum_i |F_ij F_ik| G_ii <= 2^-51 (sigma_j + sigma_k) sigma_1, so the pair's
+ * rotation error stays within ~12 units of 2^-53 sigma_1 / g.  On the pixel-derived covers of
+ * the sweep study it rejects no step the absolute test took.  All f32 IEEE operations in a
+ * fixed order: the device evaluates it bit for bit alike (and may skip the pair tests when
+ * (max q)^2 <= 128 min r, which implies every one of them in f32). */
+static int g_newton_scaled = 1;
+void orc_set_newton_scaled(int on) { g_newton_scaled = on; } /* studies only: 0 = the round-5 test */
+
+static int newton_scaled_ok(const double *G, const float *F, int b)
+{
+    double gmax = 0.0;
+    for (int k = 0; k < b; ++k) gmax = G[k] > gmax ? G[k] : gmax;
+    const float ginv = 1.0f / (float)gmax;
+    float r[ORC_MAXB], qw[ORC_MAXB];
+    for (int k = 0; k < b; ++k) {
+        r[k] = (float)G[k] * ginv;
+        qw[k] = 0.0f;
+    }
+    for (int s = 0; s < b - 1; ++s)
+        for (int p = 0; p < b / 2; ++p) {
+            int i, j;
+            jac_pairs(b, s, p, &i, &j);
+            const float x = fabsf(F[i * b + j]) * 134217728.0f, x2 = x * x; /* 2^27 |F| <= 1 */
+            qw[i] = fmaf(x2, r[j], qw[i]);
+            qw[j] = fmaf(x2, r[i], qw[j]);
+        }
+    int ok = 1;
+    for (int j = 0; j < b; ++j)
+        for (int k = j + 1; k < b; ++k) ok &= qw[j] * qw[k] <= 64.0f * (r[j] + r[k]);
+    return ok;
+}
+
 /* Returns 1 if the step was taken (the block is done). */
 static int newton_try(double *A, double *V, int b, double c2)
 {
@@ -978,6 +1018,7 @@ static int newton_try(double *A, double *V, int b, double c2)
             ok &= fabsf(f) <= NWT_APPLY; /* NaN / inf fail */
         }
     }
+    if (ok && g_newton_scaled) ok = newton_scaled_ok(G, F, b);
     if (!ok) return 0;
     apply_f(V, F, b);
     apply_f(A, F, b);

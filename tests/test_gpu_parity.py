@@ -149,6 +149,33 @@ def test_svd_blocks_gpu_bit_identical_noise_frame(dev, b):
     assert np.array_equal(sw.cpu().numpy(), swo)
 
 
+@pytest.mark.parametrize("b", ALL_B)
+def test_svd_blocks_gpu_bit_identical_graded(dev, b):
+    """The Newton finish's scaled acceptance test (round 6) on the blocks it exists
+    for -- graded spectra, near ties at the conditioning cut, clusters (tests/k_corpus.py) -- and on
+    the block that broke the certificate's bound under the round-5 test: factors, sigmas and
+    sweep counts bit-identical to the oracle, and the refused steps (blocks the round-5 test
+    would have finished by the step) really taken as sweeps on the GPU."""
+    import k_corpus as kc
+    from thatsmyface_amd import batch
+
+    D = np.concatenate([kc.dct_class(k, b, 1500, 31) for k in ("graded", "graded_diag", "near_tie", "cluster", "rank_def")])
+    if b == 8:
+        D = np.concatenate([D, np.load(os.path.join(os.path.dirname(__file__), "golden", "k_newton_outlier_b8.npy"))[None]])
+    U, S, Vt, sw = batch.svd_blocks(torch.from_numpy(D).to(dev))
+    Uo, So, Vo, swo = O.svd_blocks(D)
+    for x, y in ((S, So), (U, Uo), (Vt, Vo)):
+        assert np.array_equal(x.cpu().numpy().view(np.uint32), y.view(np.uint32))
+    assert np.array_equal(sw.cpu().numpy(), swo)
+    lib = O.lib()
+    try:
+        lib.orc_set_newton_scaled(0)
+        sw05 = O.svd_blocks(D)[3]
+    finally:
+        lib.orc_set_newton_scaled(1)
+    assert ((swo & 255) > (sw05 & 255)).any()  # the scaled test refused some steps here
+
+
 # ---------------------------------------------------------------- the dgesdd route on the GPU
 def test_lapack_nrm2_gpu(dev):
     """OpenBLAS's x87 dnrm2 (emulated in integer arithmetic) vs the oracle's long double."""
@@ -907,6 +934,62 @@ def test_hybrid_vs_reference_route_alpha_edges(dev, b):
         oh = batch.embed_batch(fr, tile, b, alpha, route="hybrid", stats=st)
         orf = batch.embed_batch(fr, tile, b, alpha, route="reference")
         assert torch.equal(oh, orf), (b, alpha, st)
+
+
+@pytest.mark.parametrize("wm", ["noise", "qr"])
+def test_rank1_route_equals_reference_route_4k(dev, wm):
+    """TMFWM_ROUTE_RANK1 (ABI 10): the rank-1 pre-pass keeps the bytes of the blocks
+    whose f32(D + c u1 v1^T) it proves equal to the reference's and sends the rest through the
+    hybrid route.  Its bytes equal the reference route's (np.linalg.svd's arithmetic on every
+    block) on camera-like 4K covers, where it decides most blocks itself, and on the bench's noise
+    covers, where most go to the list pass."""
+    import sys as _sys
+
+    _sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "exp"))
+    from route_diff_gpu import blocks_differing, photo_covers
+
+    from thatsmyface_amd import batch
+
+    b, H, W = 8, 2160, 3840
+    if wm == "qr":
+        tile = torch.from_numpy(_u8(81, (H // b, W // b)) & np.uint8(1)).to(dev) * 255
+    else:
+        tile = batch.synth_tile(H // b, W // b, device=dev)
+    for kind, n in (("photo", 16), ("noise", 4)):
+        fr = photo_covers(n, H, W, 83, dev) if kind == "photo" else batch.synth_frames(n, H, W, device=dev)
+        st = {}
+        o1 = batch.embed_batch(fr, tile, b, 0.1, route="rank1", stats=st)
+        orf = batch.embed_batch(fr, tile, b, 0.1, route="reference")
+        nb = blocks_differing(o1, orf, b)
+        assert nb == 0 and torch.equal(o1, orf), (kind, nb, st)
+        total = n * (H // b) * (W // b)
+        if kind == "photo":
+            assert st["list_pass_blocks"] < total // 2, st  # the pre-pass decided most blocks itself
+
+
+def test_rank1_route_edges(dev):
+    """The rank-1 pre-pass on its edge cases: zero (black) and flat frames (D = 0, D zero but for
+    D[0][0]), frames whose size is not a multiple of b (edge pixels), alpha = 0, large and negative
+    alpha (S'[0] < 0), a frame of noise next to camera-like ones; block sizes other than 8 take the
+    hybrid route.  Every byte equals the reference route's."""
+    import sys as _sys
+
+    _sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "exp"))
+    from route_diff_gpu import photo_covers
+
+    from thatsmyface_amd import batch
+
+    H, W = 548, 965
+    fr = photo_covers(4, H, W, 91, dev)
+    fr[1] = 0
+    fr[2] = torch.tensor([37, 140, 201], dtype=torch.uint8, device=dev)
+    fr[3] = torch.from_numpy(_u8(92, (H, W, 3))).to(dev)
+    for b in (8, 12):
+        tile = torch.from_numpy(_u8(93 + b, (H // b, W // b)) & np.uint8(1)).to(dev) * 255
+        for alpha in (0.1, 0.0, 1.0, -0.05, -5.0):
+            o1 = batch.embed_batch(fr, tile, b, alpha, route="rank1")
+            orf = batch.embed_batch(fr, tile, b, alpha, route="reference")
+            assert torch.equal(o1, orf), (b, alpha)
 
 
 @pytest.mark.parametrize("mem", ["host", "device"])

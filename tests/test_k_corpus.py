@@ -1,0 +1,68 @@
+"""The byte certificate's bound K, measured directly.
+
+The hybrid route certifies its bytes assuming LAPACK's f64 factors (np.linalg.svd at
+/root/reference/modules/watermarking.py:195) and the Jacobi route's lie within
+K 2^-53 sigma_1 / g_k of each other per element (sigma within K 2^-53 sigma_1), K = 256
+(csrc/tmfwm_blocks.h kCertScale).  These tests measure that difference itself on seeded cover
+classes (tests/k_corpus.py) and on the worst blocks of the >= 10^7-block study
+(tools/exp/k_study.py, profiles/r06/k_study/), and require at most K/2 everywhere.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import k_corpus as kc
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+HALF_K = kc.K_CERT / 2
+
+
+def _max_ratio(D):
+    cert, ru, rv, rs = kc.ratios(D)
+    return cert, float(max(ru[cert].max(initial=0), rv[cert].max(initial=0), rs[cert].max(initial=0)))
+
+
+@pytest.mark.parametrize("b", [8, 16])
+@pytest.mark.parametrize("kind", kc.PIXEL_KINDS + kc.DCT_KINDS)
+def test_seeded_corpus_within_half_k(b, kind):
+    """~10^5 blocks at b = 8 and ~2 x 10^4 at b = 16 over eleven cover classes: pixel-derived
+    (noise, camera-like, QR-module covers, flat + eps, gradients) and DCT-domain constructions
+    (near ties just above the 2^-20 cut, graded spectra, clusters, rank-deficient, DC-dominant)."""
+    n = 8000 if b == 8 else 2000
+    D = kc.corpus(kind, b, 77, n=n)
+    if kind in kc.PIXEL_KINDS and b == 16:
+        D = D[:n]
+    cert, m = _max_ratio(D)
+    assert cert.sum() > 0 or kind == "rank_def"
+    assert m <= HALF_K, (kind, b, m)
+
+
+@pytest.mark.parametrize("b", [8, 16])
+def test_study_worst_blocks_within_half_k(b):
+    """The 64 worst blocks of every class of the scale study (>= 10^6 certified blocks per class
+    and block size), kept as a fixture: still within K/2 on the oracle as built now."""
+    z = np.load(os.path.join(HERE, "golden", f"k_corpus_worst_b{b}.npz"))
+    for kind in z.files:
+        cert, m = _max_ratio(z[kind])
+        assert m <= HALF_K, (kind, b, m)
+
+
+def test_newton_scaled_test_fixes_graded_outlier():
+    """The block that broke the bound: a graded spectrum (sigma_7, sigma_8 ~ 1e-5 sigma_1) on which
+    the round-5 Newton finish (absolute |F| <= 2^-27 test) left the Jacobi route 447 units of
+    2^-53 sigma_1 / g_k off LAPACK.  With the scaled acceptance test (oracle newton_scaled_ok)
+    the step is refused and the block takes another sweep."""
+    D = np.load(os.path.join(HERE, "golden", "k_newton_outlier_b8.npy"))[None]
+    lib = kc.O.lib()
+    try:
+        lib.orc_set_newton_scaled(0)
+        _, m_old = _max_ratio(D)
+        sw_old = kc.O.svd_blocks(D)[3]
+    finally:
+        lib.orc_set_newton_scaled(1)
+    _, m_new = _max_ratio(D)
+    sw_new = kc.O.svd_blocks(D)[3]
+    assert m_old > kc.K_CERT
+    assert m_new <= 8
+    assert (sw_new[0] & 255) > (sw_old[0] & 255)  # one more f64 sweep instead of the step

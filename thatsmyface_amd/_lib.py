@@ -14,7 +14,7 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # TMFWM_LIB selects an alternative build (e.g. the phase-profile libtmfwm_stamps.so)
 LIB_PATH = os.environ.get("TMFWM_LIB") or os.path.join(_HERE, "libtmfwm.so")
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 MEM_HOST = 0
 MEM_DEVICE = 1
@@ -28,7 +28,8 @@ ERR_NODATA = -61
 
 ROUTE_HYBRID = 0  # TMFWM_ROUTE_*: the SVD route of embed / extract (include/tmfwm.h)
 ROUTE_REFERENCE = 1
-ROUTES = {"hybrid": ROUTE_HYBRID, "reference": ROUTE_REFERENCE}
+ROUTE_RANK1 = 2  # ABI 10: the hybrid route behind the rank-1 pre-pass (embed at b = 8; photo mode)
+ROUTES = {"hybrid": ROUTE_HYBRID, "reference": ROUTE_REFERENCE, "rank1": ROUTE_RANK1}
 
 # pixel layouts of tmfwm_embed_px / tmfwm_extract_px (include/tmfwm.h, ABI 8)
 PIX_RGB = 3
@@ -36,12 +37,12 @@ PIX_RGBX = 4  # PIL's in-memory mode "RGB" (R, G, B, pad)
 
 
 def route_code(route) -> int:
-    """"hybrid" / "reference" (or the TMFWM_ROUTE_* value) -> the ABI's route value."""
+    """"hybrid" / "reference" / "rank1" (or the TMFWM_ROUTE_* value) -> the ABI's route value."""
     if isinstance(route, str):
         if route not in ROUTES:
             raise ValueError(f"route must be one of {sorted(ROUTES)}, got {route!r}")
         return ROUTES[route]
-    if route not in (ROUTE_HYBRID, ROUTE_REFERENCE):
+    if route not in (ROUTE_HYBRID, ROUTE_REFERENCE, ROUTE_RANK1):
         raise ValueError(f"route {route!r}")
     return int(route)
 

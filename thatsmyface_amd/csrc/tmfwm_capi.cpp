@@ -294,7 +294,7 @@ int run_embed(EmbedArgs a, hipStream_t st, int64_t *n_lapack, bool check, uint32
     DevBuf list, slow, shards, counts;
     if (ch.cap > 0) {
         if (int rc = list.alloc((size_t)ch.cap * 4, st, "dgesdd-route block list")) return rc;
-        if (embed_defers(a.block) && route == TMFWM_ROUTE_HYBRID) {
+        if (embed_defers(a.block) && route != TMFWM_ROUTE_REFERENCE) {
             if (int rc = slow.alloc((size_t)ch.cap * 4, st, "list-pass block list")) return rc;
             if (int rc = shards.alloc((size_t)kListShards * kShardStride * 4, st, "list-pass segment counters")) return rc;
         }
@@ -327,6 +327,8 @@ int run_embed(EmbedArgs a, hipStream_t st, int64_t *n_lapack, bool check, uint32
         if (route == TMFWM_ROUTE_REFERENCE) {  // every block on the dgesdd route; the edges as always
             TMF_HIP(launch_edges(k.src, k.dst, k.nframes, k.H, k.W, k.frame_stride, k.block, st));
             TMF_HIP(launch_list_all(k.fb_list, k.fb_count, k.nframes * ch.per_frame, st));
+        } else if (route == TMFWM_ROUTE_RANK1) {  // the rank-1 pre-pass, its list pass, the edges
+            TMF_HIP(launch_embed_rank1(k, st));
         } else {
             TMF_HIP(launch_embed(k, st));
         }
@@ -356,7 +358,7 @@ int run_extract(ExtractArgs a, hipStream_t st, int64_t *n_lapack, bool check, ui
     }
     DevBuf list, slow, shards, counts;
     if (int rc = list.alloc((size_t)ch.cap * 4, st, "dgesdd-route block list")) return rc;
-    if (route == TMFWM_ROUTE_HYBRID) {
+    if (route != TMFWM_ROUTE_REFERENCE) {  // hybrid (TMFWM_ROUTE_RANK1: extract is the hybrid route)
         if (int rc = slow.alloc((size_t)ch.cap * 4, st, "list-pass block list")) return rc;
         if (int rc = shards.alloc((size_t)kListShards * kShardStride * 4, st, "list-pass segment counters")) return rc;
     }
@@ -489,7 +491,7 @@ int tmfwm_embed_route(const uint8_t *rgb, int64_t n_frames, int32_t height, int3
                       int32_t route, int64_t *n_lapack_blocks)
 {
     t_err.clear();
-    if (route != TMFWM_ROUTE_HYBRID && route != TMFWM_ROUTE_REFERENCE) return fail(TMFWM_ERR_INVALID, "route %d", route);
+    if (route != TMFWM_ROUTE_HYBRID && route != TMFWM_ROUTE_REFERENCE && route != TMFWM_ROUTE_RANK1) return fail(TMFWM_ERR_INVALID, "route %d", route);
     if (n_lapack_blocks) {
         *n_lapack_blocks = 0;
         t_list_pass = 0;  // this call's count from here on (an early return leaves 0)
@@ -562,7 +564,7 @@ int tmfwm_extract_route(const uint8_t *wm_rgb, const uint8_t *orig_rgb, int64_t 
                         void *hip_stream, int32_t route, int64_t *n_lapack_blocks)
 {
     t_err.clear();
-    if (route != TMFWM_ROUTE_HYBRID && route != TMFWM_ROUTE_REFERENCE) return fail(TMFWM_ERR_INVALID, "route %d", route);
+    if (route != TMFWM_ROUTE_HYBRID && route != TMFWM_ROUTE_REFERENCE && route != TMFWM_ROUTE_RANK1) return fail(TMFWM_ERR_INVALID, "route %d", route);
     if (n_lapack_blocks) {
         *n_lapack_blocks = 0;
         t_list_pass = 0;  // this call's count from here on (an early return leaves 0)
@@ -676,7 +678,7 @@ int tmfwm_embed_px(const uint8_t *rgb, int32_t in_pixel_bytes, int64_t in_frame_
         return tmfwm_embed_route(rgb, n_frames, height, width, in_frame_stride, wm_tile, block, alpha, out, mem_kind, hip_stream,
                                  route, n_lapack_blocks);
     }
-    if (route != TMFWM_ROUTE_HYBRID && route != TMFWM_ROUTE_REFERENCE) return fail(TMFWM_ERR_INVALID, "route %d", route);
+    if (route != TMFWM_ROUTE_HYBRID && route != TMFWM_ROUTE_REFERENCE && route != TMFWM_ROUTE_RANK1) return fail(TMFWM_ERR_INVALID, "route %d", route);
     if (n_lapack_blocks) {
         *n_lapack_blocks = 0;
         t_list_pass = 0;
@@ -755,7 +757,7 @@ int tmfwm_extract_px(const uint8_t *wm_rgb, int32_t wm_pixel_bytes, int64_t wm_f
     if (wm_pixel_bytes == TMFWM_PIX_RGB && orig_pixel_bytes == TMFWM_PIX_RGB && wm_frame_stride == orig_frame_stride)
         return tmfwm_extract_route(wm_rgb, orig_rgb, n_frames, height, width, wm_frame_stride, block, alpha, out_tiles, mem_kind,
                                    hip_stream, route, n_lapack_blocks);
-    if (route != TMFWM_ROUTE_HYBRID && route != TMFWM_ROUTE_REFERENCE) return fail(TMFWM_ERR_INVALID, "route %d", route);
+    if (route != TMFWM_ROUTE_HYBRID && route != TMFWM_ROUTE_REFERENCE && route != TMFWM_ROUTE_RANK1) return fail(TMFWM_ERR_INVALID, "route %d", route);
     if (n_lapack_blocks) {
         *n_lapack_blocks = 0;
         t_list_pass = 0;

@@ -1169,6 +1169,45 @@ constexpr float kNwtApply = 7.450580596923828e-09f;  // 2^-27
 template <int B>
 constexpr int tri(int i, int j) { return i * B - i * (i + 1) / 2 + (j - i - 1); }
 
+// The step's scaled acceptance test (round 6; oracle newton_scaled_ok): besides
+// every |F_ij| <= 2^-27, with x = 2^27 |F|, r_k = f32(G_kk) * (1 / f32(max G)) and
+// q_j = sum_i x_ij^2 r_i (an fmaf chain per column in the sweep's pair order: round s, its pair
+// (i, j) adds x^2 r_j to q_i and x^2 r_i to q_j), every pair must have q_j q_k <= 64 (r_j + r_k)
+// -- the step's second-order terms then stay on each pair's own scale (the absolute test alone
+// left graded blocks' small triplets off by up to 447 units of 2^-53 sigma_1 / g_k).  The pair
+// tests run only where the per-column screen (nwt_col_ok) does not already imply them.
+constexpr float kNwtScale = 134217728.0f;  // 2^27
+TMF_DEVI float nwt_x2(float f)
+{
+    const float x = __builtin_fabsf(f) * kNwtScale;
+    return x * x;
+}
+TMF_DEVI bool nwt_pair_ok(float qj, float qk, float rj, float rk) { return qj * qk <= 64.0f * (rj + rk); }
+// the screen: q_j^2 <= 64 r_j for every column implies every pair's test in f32 (q_j q_k <=
+// 64 sqrt(r_j r_k) <= 32 (r_j + r_k), and the factor 2 covers the roundings)
+TMF_DEVI bool nwt_col_ok(float qj, float rj) { return qj * qj <= 64.0f * rj; }
+// the gate: with x_max the block's largest 2^27 |F|, S = sum r and r_min = min r, every q_j is
+// at most x_max^2 S, so (x_max^2 S)^2 <= 32 r_min implies every column's screen (the factor 2
+// covers the f32 roundings of the q chains and of the gate); the sums are then not formed
+TMF_DEVI bool nwt_gate(float fmax_abs, float S, float rmin)
+{
+    const float x = fmax_abs * kNwtScale, t = x * x * S;
+    return t * t <= 32.0f * rmin;
+}
+// largest value over the L lanes of a group, for non-negative floats (their bit patterns order alike)
+template <int L>
+TMF_DEVI float group_max_nonneg(float v)
+{
+    int b = __builtin_bit_cast(int, v), o;
+    if constexpr (L >= 2) b = (o = dpp<0xB1>(b)) > b ? o : b;
+    if constexpr (L >= 4) b = (o = dpp<0x4E>(b)) > b ? o : b;
+    if constexpr (L >= 8) b = (o = dpp<0x141>(b)) > b ? o : b;
+    return __builtin_bit_cast(float, b);
+}
+
+template <int B>
+TMF_DEVI bool nwt_scaled_ok(const double (&G)[B], const float (&F)[B * (B - 1) / 2], float fmx, bool ok);
+
 // X <- X + f64(f32(X) F) on this lane's rows, F antisymmetric (upper triangle in F[],
 // diagonal 0): fma chain over i != j, as the oracle's apply_f().  `take` false: unchanged.
 template <int B, int L>
@@ -1214,6 +1253,44 @@ struct TriPair {
     }
 };
 
+// fmx: the block's largest |F|; ok: the absolute test passed (the result matters only then)
+template <int B>
+TMF_DEVI bool nwt_scaled_ok(const double (&G)[B], const float (&F)[B * (B - 1) / 2], float fmx, bool ok)
+{
+    double gmax = 0.0;
+#pragma unroll
+    for (int k = 0; k < B; ++k) gmax = G[k] > gmax ? G[k] : gmax;
+    const float ginv = 1.0f / (float)gmax;
+    float r[B], qw[B], sum = 0.0f, rmin = 1.0f;
+#pragma unroll
+    for (int k = 0; k < B; ++k) {
+        r[k] = (float)G[k] * ginv;
+        qw[k] = 0.0f;
+        sum += r[k];
+        rmin = __builtin_fminf(rmin, r[k]);
+    }
+    if (!__any(ok && !nwt_gate(fmx, sum, rmin))) return true;
+    static_for<B - 1>([&](auto S) {
+        static_for<B / 2>([&](auto P) {
+            constexpr int i = Sched<B>::lo(S, P), j = Sched<B>::hi(S, P);
+            const float x2 = nwt_x2(F[tri<B>(i, j)]);
+            qw[i] = __builtin_fmaf(x2, r[j], qw[i]);
+            qw[j] = __builtin_fmaf(x2, r[i], qw[j]);
+        });
+    });
+    bool pass = true;
+#pragma unroll
+    for (int k = 0; k < B; ++k) pass = pass && nwt_col_ok(qw[k], r[k]);
+    if (__any(!pass)) {
+        pass = true;
+#pragma unroll
+        for (int j = 0; j < B; ++j)
+#pragma unroll
+            for (int k = j + 1; k < B; ++k) pass = pass && nwt_pair_ok(qw[j], qw[k], r[j], r[k]);
+    }
+    return pass;
+}
+
 // F_p from the pair's dot product g and the diagonal of G, or 0 if the Jacobi's tests would
 // not rotate the pair (oracle newton_try)
 TMF_DEVI float newton_f(double g, double gi, double gj, double c2)
@@ -1235,7 +1312,7 @@ TMF_DEVI bool newton_try(double (&A)[(B + L - 1) / L][B], double (&V)[(B + L - 1
     double G[B];
     static_for<B>([&](auto K) { G[K] = cdot_part<R, B>(A, K, K); });
     static_for<B>([&](auto K) { G[K] = group_sum<L>(G[K]); });
-    float F[NP];
+    float F[NP], fmx = 0.0f;
     int ok = enable ? 1 : 0;
     if constexpr (L == 2) {
         int q = (int)(__lane_id() & 1);
@@ -1250,6 +1327,7 @@ TMF_DEVI bool newton_try(double (&A)[(B + L - 1) / L][B], double (&V)[(B + L - 1
             const double g = keep + dpp<0xB1>(send);
             const float f = newton_f(g, blend(m0, G[i0], G[i1]), blend(m0, G[j0], G[j1]), c2);
             ok &= (int)(__builtin_fabsf(f) <= kNwtApply);  // NaN / inf fail
+            fmx = __builtin_fmaxf(fmx, __builtin_fabsf(f));
             const float other = dpp<0xB1>(f);
             F[p0] = blend(m0, f, other);
             F[p1] = blend(m0, other, f);
@@ -1258,15 +1336,19 @@ TMF_DEVI bool newton_try(double (&A)[(B + L - 1) / L][B], double (&V)[(B + L - 1
             constexpr int p = NP - 1, i = TriPair<B>::i(p), j = TriPair<B>::j(p);
             F[p] = newton_f(cdot<R, B, L>(A, i, j), G[i], G[j], c2);
             ok &= (int)(__builtin_fabsf(F[p]) <= kNwtApply);
+            fmx = __builtin_fmaxf(fmx, __builtin_fabsf(F[p]));
         }
         ok &= dpp<0xB1>(ok);
+        fmx = group_max_nonneg<2>(fmx);
     } else {
         static_for<NP>([&](auto P) {
             constexpr int p = P, i = TriPair<B>::i(p), j = TriPair<B>::j(p);
             F[p] = newton_f(cdot<R, B, L>(A, i, j), G[i], G[j], c2);
             ok &= (int)(__builtin_fabsf(F[p]) <= kNwtApply);
+            fmx = __builtin_fmaxf(fmx, __builtin_fabsf(F[p]));
         });
     }
+    if (__any(ok != 0)) ok &= (int)nwt_scaled_ok<B>(G, F, fmx, ok != 0);  // every lane of the block alike
     const bool take = ok != 0;
     if (__any(take)) {
         apply_f<B, L>(V, F, take);
@@ -1335,6 +1417,10 @@ TMF_DEVI bool newton_try_lds(double (&A)[(B + L - 1) / L][B], double (&V)[(B + L
     // q through an opaque move: the per-round columns / slots derived from it would
     // otherwise be hoisted out of the sweep loop and held in registers across it
     asm volatile("" : "+v"(q));
+    // the scaled test's q_j and r_j (round 6) in the pair partials' slots, free after the rounds
+    float *qt = reinterpret_cast<float *>(part), *rt = qt + B;
+    static_assert(2 * B <= 2 * (B / 2) * L, "q, r fit the partials' slots");
+    float gsum, grmin;  // the gate's S and r_min (nwt_gate), from the diagonal of G
     {
         double G[B];
         static_for<B>([&](auto K) { G[K] = cdot_part<R, B>(A, K, K); });
@@ -1342,8 +1428,21 @@ TMF_DEVI bool newton_try_lds(double (&A)[(B + L - 1) / L][B], double (&V)[(B + L
         lds_order();
         if (q == 0) static_for<B>([&](auto K) { nl[K] = G[K]; });
         lds_order();
+        double gmax = 0.0;
+#pragma unroll
+        for (int k = 0; k < B; ++k) gmax = G[k] > gmax ? G[k] : gmax;
+        const float ginv = 1.0f / (float)gmax;
+        gsum = 0.0f;
+        grmin = 1.0f;
+#pragma unroll
+        for (int k = 0; k < B; ++k) {
+            const float r = (float)G[k] * ginv;
+            gsum += r;
+            grmin = __builtin_fminf(grmin, r);
+        }
     }
     int ok = 1;
+    float fmx = 0.0f;  // this lane's largest |F|
     static_for<B - 1>([&](auto S) {
         constexpr int s = S;
         // the rounds are independent (A is not modified): without a fence the scheduler
@@ -1367,10 +1466,73 @@ TMF_DEVI bool newton_try_lds(double (&A)[(B + L - 1) / L][B], double (&V)[(B + L
             const bool rot = has && !((g2 <= c2 * (a + b)) | (g2 <= (JacP<double>::kTol2 * a) * b));
             const float f = rot ? (float)g / (float)(b - a) : 0.0f;
             ok &= (int)(__builtin_fabsf(f) <= kNwtApply);  // NaN / inf fail
+            fmx = __builtin_fmaxf(fmx, __builtin_fabsf(f));
             if (has) Ft[s * NP + pq] = f;
         });
     });
-    const bool take = enable && group_or<L>(1 - ok) == 0;
+    ok = enable && group_or<L>(1 - ok) == 0 ? 1 : 0;
+    fmx = group_max_nonneg<L>(fmx);
+    const bool gate = nwt_gate(fmx, gsum, grmin);  // decides for the block: no sums
+    if (__any(ok != 0 && !gate)) {
+        // the scaled test: every lane reads the block's q and r (the owners' updates are done);
+        // the pair tests, if the screen does not decide, each lane on the pairs it owns
+        lds_order();  // after the owners' table writes and the last round's partial reads
+        if (q == 0) {
+            double gmax = 0.0;
+            static_for<B>([&](auto K) { gmax = nl[K] > gmax ? nl[K] : gmax; });
+            const float ginv = 1.0f / (float)gmax;
+            static_for<B>([&](auto K) {
+                rt[K] = (float)nl[K] * ginv;
+                qt[K] = 0.0f;
+            });
+        }
+        lds_order();
+        {
+            int qq = q;
+            asm volatile("" : "+v"(qq));  // the pairs' columns derived here, not hoisted
+            // q_j in the round order: each column is in one pair of a round, whose owner updates it
+            static_for<B - 1>([&](auto S) {
+                constexpr int s = S;
+                lds_order();  // after the previous round's updates
+                static_for<PP>([&](auto U) {
+                    const int pq = qq * PP + U;
+                    const int i = (int)__builtin_amdgcn_ubfe(sched_nibbles<B, s, false>(), 4 * pq, 4);
+                    const int j = (int)__builtin_amdgcn_ubfe(sched_nibbles<B, s, true>(), 4 * pq, 4);
+                    if (pq < NP) {
+                        const float x2 = nwt_x2(Ft[s * NP + pq]);
+                        qt[i] = __builtin_fmaf(x2, rt[j], qt[i]);
+                        qt[j] = __builtin_fmaf(x2, rt[i], qt[j]);
+                    }
+                });
+            });
+        }
+        lds_order();
+        int pass = 1;
+#pragma unroll
+        for (int jj = 0; jj < (B + L - 1) / L; ++jj) {
+            const int j = q + jj * L;
+            if (j < B) pass &= (int)nwt_col_ok(qt[j], rt[j]);
+        }
+        pass = group_or<L>(1 - pass) == 0 ? 1 : 0;
+        if (__any(pass == 0)) {
+            pass = 1;
+            int qq = q;
+            asm volatile("" : "+v"(qq));  // the pairs' columns derived here, not hoisted
+            static_for<B - 1>([&](auto S) {
+                constexpr int s = S;
+                lds_order();  // one round's reads at a time
+                static_for<PP>([&](auto U) {
+                    const int pq = qq * PP + U;
+                    const int i = (int)__builtin_amdgcn_ubfe(sched_nibbles<B, s, false>(), 4 * pq, 4);
+                    const int j = (int)__builtin_amdgcn_ubfe(sched_nibbles<B, s, true>(), 4 * pq, 4);
+                    if (pq < NP) pass &= (int)nwt_pair_ok(qt[i], qt[j], rt[i], rt[j]);
+                });
+            });
+            pass = group_or<L>(1 - pass) == 0 ? 1 : 0;
+        }
+        ok &= pass;
+    }
+    const bool take = ok != 0;
     if (__any(take)) {
         lds_order();  // after the owners' table writes
         apply_f_lds<B, L>(V, Ft, take);

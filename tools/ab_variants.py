@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""A/B of library variants on one box: for each variants/libtmfwm_<name>.so (built by
+"""A/B of library variants on one box: for each ab/libtmfwm_<name>.so (built by
 tools/build_variant.sh) time embed / extract on synthetic 4K frames and hash the outputs,
 alternating the variants over several rounds (boxes and clocks drift; one call, one box).
 Usage: python tools/ab_variants.py --block 16 --frames 64 --rounds 3 name1 name2 ...
@@ -60,7 +60,7 @@ def main():
     hashes = {}
     for r in range(a.rounds):
         for n in a.names:
-            env = dict(os.environ, ROOT=ROOT, TMFWM_LIB=os.path.join(ROOT, "variants", f"libtmfwm_{n}.so"))
+            env = dict(os.environ, ROOT=ROOT, TMFWM_LIB=os.path.join(ROOT, "ab", f"libtmfwm_{n}.so"))
             out = subprocess.run([sys.executable, "-c", CHILD, str(a.block), str(a.frames), a.cover], env=env, capture_output=True,
                                  text=True, timeout=300)
             if out.returncode != 0:

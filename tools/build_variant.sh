@@ -1,6 +1,6 @@
 #!/bin/bash
 # Build an experimental library variant: tools/build_variant.sh <name> [extra hipcc flags...]
-# -> variants/libtmfwm_<name>.so (git-ignored; travels to the GPU box; load it with TMFWM_LIB).
+# -> ab/libtmfwm_<name>.so (git-ignored; travels to the GPU box; load it with TMFWM_LIB).
 # The kernel TUs take the extra flags; with FALLBACK=1 in the environment the dgesdd-route
 # TU (tmfwm_fallback.hip) is recompiled with them too, otherwise the ABI / tile / QR /
 # dgesdd-route objects are the main build's (make -C thatsmyface_amd/csrc first).
@@ -46,8 +46,8 @@ if [ "${FALLBACK:-0}" = "1" ]; then
   done
 fi
 wait
-mkdir -p "$ROOT/variants"
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$ROOT/variants/libtmfwm_$NAME.so" "$T/k.o" "$T/e8.o" \
+mkdir -p "$ROOT/ab"
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$ROOT/ab/libtmfwm_$NAME.so" "$T/k.o" "$T/e8.o" \
     "$C/tmfwm_capi.o" "$C/tmfwm_multi.o" "$C/tmfwm_qr.o" "$C/tmfwm_tile.o" "$C/tmfwm_pixels.o" $FB -fopenmp -ldl -lpthread
 rm -rf "$T"
-echo "variants/libtmfwm_$NAME.so"
+echo "ab/libtmfwm_$NAME.so"

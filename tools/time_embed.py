@@ -24,7 +24,8 @@ def main():
     p.add_argument("--reps", type=int, default=3)
     p.add_argument("--kind", choices=["noise", "photo"], default="noise", help="covers: the bench's noise or camera-like")
     p.add_argument("--wm", choices=["noise", "qr"], default="noise", help="watermark tile: uniform bytes or binary (QR)")
-    p.add_argument("--route", choices=["hybrid", "reference"], default="hybrid")
+    p.add_argument("--route", choices=["hybrid", "reference", "rank1"], default="hybrid")
+    p.add_argument("--hash", action="store_true", help="sha256 of the embed output and the extracted tiles (A/B identity)")
     a = p.parse_args()
     dev = torch.device("cuda", 0)
     b = a.block
@@ -48,8 +49,13 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         res[name] = round(e0.elapsed_time(e1) * 1000 / a.reps / a.frames, 2)
-    print(json.dumps({"lib": os.path.basename(os.environ.get("TMFWM_LIB", "libtmfwm.so")), "block": b, "kind": a.kind, "wm": a.wm,
-                      "route": rt, "frames": a.frames, "dgesdd_route_blocks": st.get("lapack_blocks"), "us_per_frame": res}))
+    line = {"lib": os.path.basename(os.environ.get("TMFWM_LIB", "libtmfwm.so")), "block": b, "kind": a.kind, "wm": a.wm,
+            "route": rt, "frames": a.frames, "dgesdd_route_blocks": st.get("lapack_blocks"), "us_per_frame": res}
+    if a.hash:
+        import hashlib
+        line["sha256"] = {"embed": hashlib.sha256(out.cpu().numpy().tobytes()).hexdigest()[:16],
+                          "extract": hashlib.sha256(ext.cpu().numpy().tobytes()).hexdigest()[:16]}
+    print(json.dumps(line))
 
 
 if __name__ == "__main__":
