@@ -69,9 +69,14 @@ def parse(argv=None):
                         "a differing byte fails the run (exit status 3)")
     p.add_argument("--pg-timeout", type=float, default=600.0,
                    help="seconds a rank may wait in a collective before the run fails (N > 1)")
-    p.add_argument("--route", default="hybrid", choices=["hybrid", "reference"],
-                   help="SVD route (DESIGN.md 3.5): hybrid = Jacobi + conditioning test (the throughput route); "
-                        "reference = the dgesdd route for every block (np.linalg.svd's arithmetic by construction)")
+    p.add_argument("--route", default="hybrid", choices=["hybrid", "reference", "rank1"],
+                   help="SVD route (DESIGN.md 3.5): hybrid = Jacobi + byte certificate (the throughput route); "
+                        "reference = the dgesdd route for every block (np.linalg.svd's arithmetic by construction); "
+                        "rank1 = the hybrid route behind the rank-1 pre-pass (b = 8, photo mode, DESIGN.md 5)")
+    p.add_argument("--covers", default="noise", choices=["noise", "photo"],
+                   help="synthetic covers: uniform bytes (configs[1]-[4], the default) or camera-like frames")
+    p.add_argument("--wm", default="noise", choices=["noise", "qr"],
+                   help="synthetic watermark tile: uniform bytes (the default) or a binary QR-style tile")
     p.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                    help="process-group backend for N > 1 (nccl = RCCL over xGMI; gloo only to rehearse "
                         "several ranks on one GPU)")
@@ -153,17 +158,23 @@ def spawn_ranks(args, argv, script=None) -> int:
     return subprocess.call(cmd, env=env)
 
 
-def gpu_kernels(route="hybrid"):
-    """The product path: libtmfwm.so's HIP kernels (thatsmyface_amd.batch)."""
+def gpu_kernels(route="hybrid", covers="noise", wm="noise"):
+    """The product path: libtmfwm.so's HIP kernels (thatsmyface_amd.batch).  covers / wm: the
+    synthetic inputs (noise bytes, the default; or camera-like frames and a binary QR-style tile)."""
     from thatsmyface_amd import batch
 
+    if covers == "photo":
+        synth = lambda n, h, w, frame0, dev: batch.synth_photo_frames(n, h, w, seed=batch.SEED_COVER, frame0=frame0, device=dev)  # noqa: E731
+    else:
+        synth = lambda n, h, w, frame0, dev: batch.synth_frames(n, h, w, seed=batch.SEED_COVER, frame0=frame0, device=dev)  # noqa: E731
     return SimpleNamespace(
-        synth_frames=lambda n, h, w, frame0, dev: batch.synth_frames(n, h, w, seed=batch.SEED_COVER, frame0=frame0, device=dev),
-        synth_tile=lambda nbh, nbw, dev: batch.synth_tile(nbh, nbw, device=dev),
+        synth_frames=synth,
+        synth_tile=(lambda nbh, nbw, dev: batch.synth_qr_tile(nbh, nbw, device=dev)) if wm == "qr" else
+                   (lambda nbh, nbw, dev: batch.synth_tile(nbh, nbw, device=dev)),
         embed=lambda f, t, b, a, o: batch.embed_batch(f, t, b, a, out=o, route=route),
         extract=lambda w_, o_, b, a, out: batch.extract_batch(w_, o_, b, a, out=out, route=route),
         embed_stats=lambda f, t, b, a, o: (lambda st: (batch.embed_batch(f, t, b, a, out=o, stats=st, route=route), st)[1])({}),
-        embed_list_pass=lambda b: batch.embed_list_pass(b) and route == "hybrid",
+        embed_list_pass=lambda b: batch.embed_list_pass(b) and route != "reference",
         route=route,
         exact_embed=lambda f, t, b, a, o: batch.embed_batch(f, t, b, a, out=o, route="reference"),
         exact_extract=lambda w_, o_, b, a, out: batch.extract_batch(w_, o_, b, a, out=out, route="reference"),
@@ -351,7 +362,7 @@ def run(args, kernels=None, device=None):
             dist.init_process_group("nccl", device_id=dev, timeout=timeout)
         else:
             dist.init_process_group("gloo", timeout=timeout)
-    K = kernels or gpu_kernels(getattr(args, "route", "hybrid"))
+    K = kernels or gpu_kernels(getattr(args, "route", "hybrid"), getattr(args, "covers", "noise"), getattr(args, "wm", "noise"))
     sync = torch.cuda.synchronize if on_gpu else (lambda: None)
 
     # distinct physical devices across ranks
@@ -435,7 +446,7 @@ def run(args, kernels=None, device=None):
 
     # every rank compares its timed output with the reference route (all of it by default)
     exact = None
-    if getattr(K, "route", "hybrid") == "hybrid" and args.exact_frames != 0:
+    if getattr(K, "route", "hybrid") != "reference" and args.exact_frames != 0:
         exact = exact_route_check(K, frames, wm, rt.out, rt.tiles, b, alpha, args.exact_frames, on_gpu)
         if world > 1:
             cdev = dev if args.backend == "nccl" else "cpu"
@@ -602,9 +613,13 @@ def run(args, kernels=None, device=None):
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64+f32 (u8 I/O)",
-            "data": "synthetic (splitmix64 uniform u8 covers + tile, generated in HBM)",
+            "data": ("synthetic (splitmix64 uniform u8 covers + tile, generated in HBM)"
+                     if getattr(args, "covers", "noise") == "noise" and getattr(args, "wm", "noise") == "noise" else
+                     f"synthetic ({getattr(args, 'covers', 'noise')} covers, {getattr(args, 'wm', 'noise')} tile, generated in HBM)"),
             "config": {
-                "workload": workload_name(F, H, W, b, alpha, world),
+                "workload": workload_name(F, H, W, b, alpha, world) + (
+                    "" if getattr(args, "covers", "noise") == "noise" and getattr(args, "wm", "noise") == "noise" else
+                    f" [{getattr(args, 'covers', 'noise')} covers, {getattr(args, 'wm', 'noise')} watermark]"),
                 "frames_per_gpu": F,
                 "frames_total": F * world,
                 "height": H,

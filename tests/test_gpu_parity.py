@@ -941,8 +941,9 @@ def test_rank1_route_equals_reference_route_4k(dev, wm):
     """TMFWM_ROUTE_RANK1 (ABI 10): the rank-1 pre-pass keeps the bytes of the blocks
     whose f32(D + c u1 v1^T) it proves equal to the reference's and sends the rest through the
     hybrid route.  Its bytes equal the reference route's (np.linalg.svd's arithmetic on every
-    block) on camera-like 4K covers, where it decides most blocks itself, and on the bench's noise
-    covers, where most go to the list pass."""
+    block) on camera-like 4K covers, where it decides most blocks itself under a continuous
+    watermark (under a binary one the w = 0 blocks sit on truncation boundaries and go to the list
+    pass), and on the bench's noise covers, where most go to the list pass."""
     import sys as _sys
 
     _sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "exp"))
@@ -963,7 +964,7 @@ def test_rank1_route_equals_reference_route_4k(dev, wm):
         nb = blocks_differing(o1, orf, b)
         assert nb == 0 and torch.equal(o1, orf), (kind, nb, st)
         total = n * (H // b) * (W // b)
-        if kind == "photo":
+        if kind == "photo" and wm == "noise":
             assert st["list_pass_blocks"] < total // 2, st  # the pre-pass decided most blocks itself
 
 

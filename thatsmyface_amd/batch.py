@@ -116,6 +116,51 @@ def synth_frames(n: int, height: int, width: int, seed: int = SEED_COVER, frame0
     return out
 
 
+def synth_photo_frames(n: int, height: int, width: int, seed: int = SEED_COVER, frame0: int = 0,
+                       device: torch.device | str | None = None, chunk: int = 16) -> torch.Tensor:
+    """Camera-like synthetic uint8 frames (tests/lapack_path.photo_cover's recipe on the device:
+    a low-pass field + gradients + fine grain, the decaying DCT spectra of natural images),
+    generated `chunk` frames at a time with one generator seed per frame (seed + frame index)."""
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    out = torch.empty((n, height, width, 3), dtype=torch.uint8, device=dev)
+    y = torch.linspace(0, 1, height, device=dev).view(1, height, 1, 1)
+    x = torch.linspace(0, 1, width, device=dev).view(1, 1, width, 1)
+    for c0 in range(0, n, chunk):
+        k = min(chunk, n - c0)
+        f = torch.empty((k, height // 16 + 2, width // 16 + 2, 3), device=dev)
+        g = torch.Generator(device=dev)
+        for i in range(k):
+            g.manual_seed(seed + frame0 + c0 + i)
+            f[i] = torch.randn(f.shape[1:], generator=g, device=dev)
+        f = f.repeat_interleave(16, 1).repeat_interleave(16, 2)[:, :height, :width]
+        for ax in (1, 2):
+            for _ in range(2):
+                f = (torch.roll(f, 5, ax) + torch.roll(f, -5, ax) + f) / 3.0
+        img = 128 + 45 * f + 60 * (x - 0.5) + 30 * (y - 0.5)
+        g.manual_seed(seed + frame0 + c0 + 0x9E3779B9)
+        img += 2.0 * torch.randn(img.shape, generator=g, device=dev)
+        out[c0:c0 + k] = img.clamp_(0, 255).to(torch.uint8)
+    return out
+
+
+def synth_qr_tile(nbh: int, nbw: int, seed: int = SEED_WATERMARK, device=None) -> torch.Tensor:
+    """The app's watermark tile: a QR code of a 48-byte payload (an AES-CBC ciphertext's size:
+    IV + two blocks, base64 in the symbol, level H) rendered by text_to_qrcode (300 x 300) and
+    resized to the block grid by resize_watermark with preserve_ratio=True, as the embed page does
+    (embed_watermark_page.py:492-531; modules/qrcode_generator.py:10-44): 0 / 255 modules with
+    LANCZOS edges, centred on a white canvas."""
+    import numpy as np  # noqa: PLC0415
+
+    from . import qrcode_generator, watermarking  # noqa: PLC0415
+
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    payload = np.random.default_rng(seed).integers(0, 256, 48).astype(np.uint8).tobytes()
+    img = qrcode_generator.text_to_qrcode(payload)
+    with torch.cuda.device(dev):
+        t = np.asarray(watermarking.resize_watermark(img, nbh, nbw, preserve_ratio=True), dtype=np.uint8)
+    return torch.from_numpy(np.ascontiguousarray(t)).to(dev)
+
+
 def synth_tile(nbh: int, nbw: int, seed: int = SEED_WATERMARK, device=None) -> torch.Tensor:
     """Synthetic watermark tile: the same generator over an nbh x nbw byte plane."""
     dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())

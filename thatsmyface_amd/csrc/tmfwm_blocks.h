@@ -262,9 +262,6 @@ template <int B>
 constexpr int kEmbedTS = B == 8 ? 73 : B == 16 ? kEmbedTS1<B> + ((24 - kEmbedTS1<B> % 32) + 32) % 32 : kEmbedTS1<B>;
 static_assert(kEmbedTS<8> >= kEmbedTS1<8> && kEmbedTS<16> % 32 == 24, "tile strides");
 
-#ifndef TMF_ONE_BALLOT
-#define TMF_ONE_BALLOT 0
-#endif
 // Byte certificate of the hybrid route (oracle tmfwm_cert.cpp): LAPACK's f64
 // factors lie within E_k = kCertScale s1 / g_k of the Jacobi route's, every singular value
 // within kCertScale s1 (K = 256 units of 2^-53 s1 / g_k; LAPACK's own V is off by up to 94,
@@ -301,12 +298,6 @@ constexpr bool kReloadBytes = B == 16;
 // embed<10> 271 -> 247).  At b = 8 / 16 the free schedule is faster (128 vs 139 us, 334 vs 364).
 template <int B>
 constexpr bool kPinChain = B == 10 || B == 14;
-
-// The inverse colour's end-point test decides with one wave-uniform branch per pixel row (a lane
-// mask of the row's pixels that need their upper end's bytes) instead of a branch per pixel
-// (32 per lane at b = 8, each with its exec-mask bookkeeping)
-template <int B>
-constexpr bool kOneBallot = TMF_ONE_BALLOT;
 
 // One wave's blocks: strip mode (LIST = false: the strip of blockIdx) or list mode (pos and
 // id from the slow list).  id = (frame * nbh + bi) * nbw + bj, relative to a.src.
@@ -560,7 +551,6 @@ TMF_DEVI void embed_blocks(const EmbedArgs &a, const StripPos &pos, uint32_t id,
     // :207-216 write back and ycbcr_to_rgb with this lane's original chroma: the lower ends'
     // bytes; a pixel whose ends give other bytes leaves the block undecided
     bool unc = neg;
-    uint32_t wmask = 0;  // kOneBallot: bit c set for a pixel of the row whose ends may differ
     if (pos.valid && !slow) {
         if constexpr (kReloadBytes<B>) load_block_rows<B>(src, a.W, pos, q, a.aligned, words);
 #pragma unroll
@@ -583,9 +573,7 @@ TMF_DEVI void embed_blocks(const EmbedArgs &a, const StripPos &pos, uint32_t id,
                 // are the upper end's bytes computed
                 const float dy = Mh[r][c] - Ml[r][c];
                 const bool wide = dy != 0.0f && fr + __builtin_fmaf(dy, 255.1f, 0x1p-14f) >= 1.0f;
-                if constexpr (kOneBallot<B>) {
-                    wmask |= (uint32_t)wide << c;
-                } else if (__builtin_amdgcn_ballot_w64(wide) != 0 && wide) {
+                if (__builtin_amdgcn_ballot_w64(wide) != 0 && wide) {
                     uint32_t R9, G9, B9;
                     colour_inv(Mh[r][c], cbs, crs, R9, G9, B9);
                     unc = unc || R9 != R8 || G9 != G8 || B9 != B8;
@@ -594,25 +582,6 @@ TMF_DEVI void embed_blocks(const EmbedArgs &a, const StripPos &pos, uint32_t id,
                 out[k0 >> 2] |= R8 << (8 * (k0 & 3));
                 out[(k0 + 1) >> 2] |= G8 << (8 * ((k0 + 1) & 3));
                 out[(k0 + 2) >> 2] |= B8 << (8 * ((k0 + 2) & 3));
-            }
-            if constexpr (kOneBallot<B>) {
-                // the row's pixels whose ends may give other bytes: one wave-uniform test per row
-                // (nearly never taken), then both ends' bytes of each such pixel
-                if (__builtin_amdgcn_ballot_w64(wmask != 0) != 0) {
-#pragma unroll
-                    for (int c = 0; c < B; ++c)
-                        if ((wmask >> c) & 1u) {
-                            float cbs, crs;
-                            const uint32_t R0 = byte_at(words[r], 3 * c), G0 = byte_at(words[r], 3 * c + 1),
-                                           B0 = byte_at(words[r], 3 * c + 2);
-                            chroma(R0, G0, B0, cbs, crs);
-                            uint32_t R8, G8, B8, R9, G9, B9;
-                            colour_inv(Ml[r][c], cbs, crs, R8, G8, B8);
-                            colour_inv(Mh[r][c], cbs, crs, R9, G9, B9);
-                            unc = unc || R9 != R8 || G9 != G8 || B9 != B8;
-                        }
-                }
-                wmask = 0;
             }
             uint8_t *p = dst + ((int64_t)(pos.bi * B + q * R + r) * a.W + (int64_t)pos.bj * B) * 3;
             if (real_row<B>(q, r)) store_words<B>(p, a.aligned, out);
