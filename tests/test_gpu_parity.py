@@ -936,8 +936,9 @@ def test_hybrid_vs_reference_route_alpha_edges(dev, b):
         assert torch.equal(oh, orf), (b, alpha, st)
 
 
+@pytest.mark.parametrize("b", [8, 16])
 @pytest.mark.parametrize("wm", ["noise", "qr"])
-def test_rank1_route_equals_reference_route_4k(dev, wm):
+def test_rank1_route_equals_reference_route_4k(dev, wm, b):
     """TMFWM_ROUTE_RANK1 (ABI 10): the rank-1 pre-pass keeps the bytes of the blocks
     whose f32(D + c u1 v1^T) it proves equal to the reference's and sends the rest through the
     hybrid route.  Its bytes equal the reference route's (np.linalg.svd's arithmetic on every
@@ -951,7 +952,7 @@ def test_rank1_route_equals_reference_route_4k(dev, wm):
 
     from thatsmyface_amd import batch
 
-    b, H, W = 8, 2160, 3840
+    H, W = 2160, 3840
     if wm == "qr":
         tile = torch.from_numpy(_u8(81, (H // b, W // b)) & np.uint8(1)).to(dev) * 255
     else:
@@ -971,8 +972,8 @@ def test_rank1_route_equals_reference_route_4k(dev, wm):
 def test_rank1_route_edges(dev):
     """The rank-1 pre-pass on its edge cases: zero (black) and flat frames (D = 0, D zero but for
     D[0][0]), frames whose size is not a multiple of b (edge pixels), alpha = 0, large and negative
-    alpha (S'[0] < 0), a frame of noise next to camera-like ones; block sizes other than 8 take the
-    hybrid route.  Every byte equals the reference route's."""
+    alpha (S'[0] < 0), a frame of noise next to camera-like ones, at b = 8 and 16; other block sizes
+    take the hybrid route.  Every byte equals the reference route's."""
     import sys as _sys
 
     _sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "exp"))
@@ -985,7 +986,7 @@ def test_rank1_route_edges(dev):
     fr[1] = 0
     fr[2] = torch.tensor([37, 140, 201], dtype=torch.uint8, device=dev)
     fr[3] = torch.from_numpy(_u8(92, (H, W, 3))).to(dev)
-    for b in (8, 12):
+    for b in (8, 12, 16):
         tile = torch.from_numpy(_u8(93 + b, (H // b, W // b)) & np.uint8(1)).to(dev) * 255
         for alpha in (0.1, 0.0, 1.0, -0.05, -5.0):
             o1 = batch.embed_batch(fr, tile, b, alpha, route="rank1")

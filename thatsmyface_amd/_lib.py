@@ -28,7 +28,7 @@ ERR_NODATA = -61
 
 ROUTE_HYBRID = 0  # TMFWM_ROUTE_*: the SVD route of embed / extract (include/tmfwm.h)
 ROUTE_REFERENCE = 1
-ROUTE_RANK1 = 2  # ABI 10: the hybrid route behind the rank-1 pre-pass (embed at b = 8; photo mode)
+ROUTE_RANK1 = 2  # ABI 10: the hybrid route behind the rank-1 pre-pass (embed at b = 8, 16; photo mode)
 ROUTES = {"hybrid": ROUTE_HYBRID, "reference": ROUTE_REFERENCE, "rank1": ROUTE_RANK1}
 
 # pixel layouts of tmfwm_embed_px / tmfwm_extract_px (include/tmfwm.h, ABI 8)

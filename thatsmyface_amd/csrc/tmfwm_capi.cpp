@@ -294,7 +294,7 @@ int run_embed(EmbedArgs a, hipStream_t st, int64_t *n_lapack, bool check, uint32
     DevBuf list, slow, shards, counts;
     if (ch.cap > 0) {
         if (int rc = list.alloc((size_t)ch.cap * 4, st, "dgesdd-route block list")) return rc;
-        if (embed_defers(a.block) && route != TMFWM_ROUTE_REFERENCE) {
+        if ((embed_defers(a.block) && route != TMFWM_ROUTE_REFERENCE) || (route == TMFWM_ROUTE_RANK1 && rank1_block(a.block))) {
             if (int rc = slow.alloc((size_t)ch.cap * 4, st, "list-pass block list")) return rc;
             if (int rc = shards.alloc((size_t)kListShards * kShardStride * 4, st, "list-pass segment counters")) return rc;
         }

@@ -93,6 +93,7 @@ int sum_sink(const uint32_t *sink, int64_t nchunks, int64_t *lapack);  // TMFWM_
 
 hipError_t launch_embed(const EmbedArgs &a, hipStream_t st);
 hipError_t launch_embed_rank1(EmbedArgs a, hipStream_t st);  // TMFWM_ROUTE_RANK1 (tmfwm_rank1.hip)
+bool rank1_block(int block);  // the block sizes TMFWM_ROUTE_RANK1 has a pre-pass for
 bool embed_defers(int block);  // the strip pass of embed_kernel<block> can leave blocks to a list pass
 hipError_t launch_edges(const uint8_t *src, uint8_t *dst, int64_t nframes, int H, int W, int64_t frame_stride, int block, hipStream_t st);
 hipError_t launch_extract(const ExtractArgs &a, hipStream_t st);

@@ -30,8 +30,11 @@
 namespace tmf {
 
 extern template __global__ void embed_kernel<8, true>(EmbedArgs);  // tmfwm_embed8.hip
+// the list pass of b = 16 exists for this route only (the hybrid route's strip pass at b = 16 runs
+// every block to the end, kDeferMax<16> = 0): instantiated here
+template __global__ void embed_kernel<16, true>(EmbedArgs);
 
-// |C[p][i]| of the orthonormal DCT-III (IDCT) of length 8, rounded up to f32
+// |C[p][i]| of the orthonormal DCT-III (IDCT) of length b, rounded up to f32
 template <int B>
 struct AbsIdct;
 template <>
@@ -48,6 +51,28 @@ struct AbsIdct<8> {
     };
 };
 
+template <>
+struct AbsIdct<16> {
+    static constexpr float m[16][16] = {
+        {2.500000298e-01f, 3.518509567e-01f, 3.467600048e-01f, 3.383295238e-01f, 3.266407847e-01f, 3.118062913e-01f, 2.939689159e-01f, 2.733004987e-01f, 2.500000298e-01f, 2.242919058e-01f, 1.964237541e-01f, 1.666639298e-01f, 1.352990419e-01f, 1.026311368e-01f, 6.897485256e-02f, 3.465429693e-02f},
+        {2.500000298e-01f, 3.383295238e-01f, 2.939689159e-01f, 2.242919058e-01f, 1.352990419e-01f, 3.465429693e-02f, 6.897485256e-02f, 1.666639298e-01f, 2.500000298e-01f, 3.118062913e-01f, 3.467600048e-01f, 3.518509567e-01f, 3.266407847e-01f, 2.733004987e-01f, 1.964237541e-01f, 1.026311368e-01f},
+        {2.500000298e-01f, 3.118062913e-01f, 1.964237541e-01f, 3.465429693e-02f, 1.352990419e-01f, 2.733004987e-01f, 3.467600048e-01f, 3.383295238e-01f, 2.500000298e-01f, 1.026311368e-01f, 6.897485256e-02f, 2.242919058e-01f, 3.266407847e-01f, 3.518509567e-01f, 2.939689159e-01f, 1.666639298e-01f},
+        {2.500000298e-01f, 2.733004987e-01f, 6.897485256e-02f, 1.666639298e-01f, 3.266407847e-01f, 3.383295238e-01f, 1.964237541e-01f, 3.465429693e-02f, 2.500000298e-01f, 3.518509567e-01f, 2.939689159e-01f, 1.026311368e-01f, 1.352990419e-01f, 3.118062913e-01f, 3.467600048e-01f, 2.242919058e-01f},
+        {2.500000298e-01f, 2.242919058e-01f, 6.897485256e-02f, 3.118062913e-01f, 3.266407847e-01f, 1.026311368e-01f, 1.964237541e-01f, 3.518509567e-01f, 2.500000298e-01f, 3.465429693e-02f, 2.939689159e-01f, 3.383295238e-01f, 1.352990419e-01f, 1.666639298e-01f, 3.467600048e-01f, 2.733004987e-01f},
+        {2.500000298e-01f, 1.666639298e-01f, 1.964237541e-01f, 3.518509567e-01f, 1.352990419e-01f, 2.242919058e-01f, 3.467600048e-01f, 1.026311368e-01f, 2.500000298e-01f, 3.383295238e-01f, 6.897485256e-02f, 2.733004987e-01f, 3.266407847e-01f, 3.465429693e-02f, 2.939689159e-01f, 3.118062913e-01f},
+        {2.500000298e-01f, 1.026311368e-01f, 2.939689159e-01f, 2.733004987e-01f, 1.352990419e-01f, 3.518509567e-01f, 6.897485256e-02f, 3.118062913e-01f, 2.500000298e-01f, 1.666639298e-01f, 3.467600048e-01f, 3.465429693e-02f, 3.266407847e-01f, 2.242919058e-01f, 1.964237541e-01f, 3.383295238e-01f},
+        {2.500000298e-01f, 3.465429693e-02f, 3.467600048e-01f, 1.026311368e-01f, 3.266407847e-01f, 1.666639298e-01f, 2.939689159e-01f, 2.242919058e-01f, 2.500000298e-01f, 2.733004987e-01f, 1.964237541e-01f, 3.118062913e-01f, 1.352990419e-01f, 3.383295238e-01f, 6.897485256e-02f, 3.518509567e-01f},
+        {2.500000298e-01f, 3.465429693e-02f, 3.467600048e-01f, 1.026311368e-01f, 3.266407847e-01f, 1.666639298e-01f, 2.939689159e-01f, 2.242919058e-01f, 2.500000298e-01f, 2.733004987e-01f, 1.964237541e-01f, 3.118062913e-01f, 1.352990419e-01f, 3.383295238e-01f, 6.897485256e-02f, 3.518509567e-01f},
+        {2.500000298e-01f, 1.026311368e-01f, 2.939689159e-01f, 2.733004987e-01f, 1.352990419e-01f, 3.518509567e-01f, 6.897485256e-02f, 3.118062913e-01f, 2.500000298e-01f, 1.666639298e-01f, 3.467600048e-01f, 3.465429693e-02f, 3.266407847e-01f, 2.242919058e-01f, 1.964237541e-01f, 3.383295238e-01f},
+        {2.500000298e-01f, 1.666639298e-01f, 1.964237541e-01f, 3.518509567e-01f, 1.352990419e-01f, 2.242919058e-01f, 3.467600048e-01f, 1.026311368e-01f, 2.500000298e-01f, 3.383295238e-01f, 6.897485256e-02f, 2.733004987e-01f, 3.266407847e-01f, 3.465429693e-02f, 2.939689159e-01f, 3.118062913e-01f},
+        {2.500000298e-01f, 2.242919058e-01f, 6.897485256e-02f, 3.118062913e-01f, 3.266407847e-01f, 1.026311368e-01f, 1.964237541e-01f, 3.518509567e-01f, 2.500000298e-01f, 3.465429693e-02f, 2.939689159e-01f, 3.383295238e-01f, 1.352990419e-01f, 1.666639298e-01f, 3.467600048e-01f, 2.733004987e-01f},
+        {2.500000298e-01f, 2.733004987e-01f, 6.897485256e-02f, 1.666639298e-01f, 3.266407847e-01f, 3.383295238e-01f, 1.964237541e-01f, 3.465429693e-02f, 2.500000298e-01f, 3.518509567e-01f, 2.939689159e-01f, 1.026311368e-01f, 1.352990419e-01f, 3.118062913e-01f, 3.467600048e-01f, 2.242919058e-01f},
+        {2.500000298e-01f, 3.118062913e-01f, 1.964237541e-01f, 3.465429693e-02f, 1.352990419e-01f, 2.733004987e-01f, 3.467600048e-01f, 3.383295238e-01f, 2.500000298e-01f, 1.026311368e-01f, 6.897485256e-02f, 2.242919058e-01f, 3.266407847e-01f, 3.518509567e-01f, 2.939689159e-01f, 1.666639298e-01f},
+        {2.500000298e-01f, 3.383295238e-01f, 2.939689159e-01f, 2.242919058e-01f, 1.352990419e-01f, 3.465429693e-02f, 6.897485256e-02f, 1.666639298e-01f, 2.500000298e-01f, 3.118062913e-01f, 3.467600048e-01f, 3.518509567e-01f, 3.266407847e-01f, 2.733004987e-01f, 1.964237541e-01f, 1.026311368e-01f},
+        {2.500000298e-01f, 3.518509567e-01f, 3.467600048e-01f, 3.383295238e-01f, 3.266407847e-01f, 3.118062913e-01f, 2.939689159e-01f, 2.733004987e-01f, 2.500000298e-01f, 2.242919058e-01f, 1.964237541e-01f, 1.666639298e-01f, 1.352990419e-01f, 1.026311368e-01f, 6.897485256e-02f, 3.465429693e-02f},
+    };
+};
+
 constexpr int kRank1Iters = 4;  // f64 power steps before the a-posteriori test
 
 // value of element k (0 <= k < B) of a per-row quantity held as R rows per lane (lane k / R)
@@ -59,10 +84,10 @@ TMF_DEVI float row_value(const float (&own)[kRows<B, L>])
 }
 
 template <int B>
-__global__ __launch_bounds__(64, 3) void embed_rank1_kernel(EmbedArgs a)
+__global__ __launch_bounds__(64, B == 8 ? 3 : 2) void embed_rank1_kernel(EmbedArgs a)
 {
     constexpr int L = Geo<B>::L, R = Geo<B>::R, BPW = Geo<B>::BPW, LD = B + 1, NW = Geo<B>::NW;
-    static_assert(B == 8, "the rank-1 pre-pass is built for b = 8");
+    static_assert(B == 8 || B == 16, "the rank-1 pre-pass is built for b = 8 and 16");
     constexpr double u53 = 1.1102230246251565e-16;  // 2^-53
     constexpr float u24 = 5.9604644775390625e-08f;  // 2^-24
     __shared__ float lds[BPW * B * LD];
@@ -290,26 +315,35 @@ __global__ __launch_bounds__(64, 3) void embed_rank1_kernel(EmbedArgs a)
     }
 }
 
-// TMFWM_ROUTE_RANK1 at b = 8: the pre-pass over every block, the list pass (embed_kernel<8, true>:
-// the full hybrid route) over the blocks it left, the edge pixels; the caller runs the dgesdd-route
-// fixup as for the hybrid route
+template <int B>
+static hipError_t launch_rank1_b(EmbedArgs a, hipStream_t st)
+{
+    a.strips_per_row = (a.nbw + Geo<B>::BPW - 1) / Geo<B>::BPW;
+    const int64_t gx = (int64_t)a.strips_per_row * a.nbh;
+    for (int64_t f0 = 0; f0 < a.nframes; f0 += 65535) {
+        EmbedArgs c = a;
+        const int64_t nf = a.nframes - f0 < 65535 ? a.nframes - f0 : 65535;
+        c.src = a.src + f0 * a.frame_stride;
+        c.dst = a.dst + f0 * a.frame_stride;
+        hipLaunchKernelGGL((embed_rank1_kernel<B>), dim3((unsigned)gx, (unsigned)nf), dim3(64), 0, st, c);
+    }
+    const int64_t rows = a.nframes * a.nbh;
+    const unsigned grid = (unsigned)(rows < (int64_t)kListShards ? rows : (int64_t)kListShards);
+    hipLaunchKernelGGL((embed_kernel<B, true>), dim3(grid), dim3(64), 0, st, a);
+    return hipGetLastError();
+}
+
+bool rank1_block(int block) { return block == 8 || block == 16; }
+
+// TMFWM_ROUTE_RANK1 at b = 8 / 16: the pre-pass over every block, the list pass (embed_kernel<b,
+// true>: the full hybrid route) over the blocks it left, the edge pixels; the caller runs the
+// dgesdd-route fixup as for the hybrid route.  Other block sizes: the hybrid route.
 hipError_t launch_embed_rank1(EmbedArgs a, hipStream_t st)
 {
-    if (a.block != 8 || !a.slow_list) return launch_embed(a, st);
+    if (!rank1_block(a.block) || !a.slow_list) return launch_embed(a, st);
     if (a.nbh > 0 && a.nbw > 0) {
-        a.strips_per_row = (a.nbw + Geo<8>::BPW - 1) / Geo<8>::BPW;
-        const int64_t gx = (int64_t)a.strips_per_row * a.nbh;
-        for (int64_t f0 = 0; f0 < a.nframes; f0 += 65535) {
-            EmbedArgs c = a;
-            const int64_t nf = a.nframes - f0 < 65535 ? a.nframes - f0 : 65535;
-            c.src = a.src + f0 * a.frame_stride;
-            c.dst = a.dst + f0 * a.frame_stride;
-            hipLaunchKernelGGL((embed_rank1_kernel<8>), dim3((unsigned)gx, (unsigned)nf), dim3(64), 0, st, c);
-        }
-        const int64_t rows = a.nframes * a.nbh;
-        const unsigned grid = (unsigned)(rows < (int64_t)kListShards ? rows : (int64_t)kListShards);
-        hipLaunchKernelGGL((embed_kernel<8, true>), dim3(grid), dim3(64), 0, st, a);
-        if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+        const hipError_t e = a.block == 8 ? launch_rank1_b<8>(a, st) : launch_rank1_b<16>(a, st);
+        if (e != hipSuccess) return e;
     }
     return launch_edges(a.src, a.dst, a.nframes, a.H, a.W, a.frame_stride, a.block, st);
 }
