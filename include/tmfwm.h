@@ -57,6 +57,12 @@ extern "C" {
                                    block whose f32(D + c u1 v1^T) it proves equal to the reference's
                                    (photo mode) and sends the rest through the hybrid
                                    route; other block sizes and extract: TMFWM_ROUTE_HYBRID */
+#define TMFWM_ROUTE_RANK1_REFERENCE 3 /* (ABI 10) the same pre-pass in front of the dgesdd route: no
+                                   Jacobi SVD and so no K -- embed rests on the pre-pass's rank-one
+                                   bound (its constants on LAPACK's residual and top pair enter
+                                   scaled by ~2^-24), extract on the certified sigma_1 enclosure
+                                   (TMFWM_ROUTE_HYBRID's extract); other block sizes: the dgesdd
+                                   route for every block */
 
 #define TMFWM_OK 0
 #define TMFWM_ERR_INVALID (-22)     /* bad argument (EINVAL) */

@@ -58,7 +58,7 @@ def test_argument_validation_before_device():
     with pytest.raises(ValueError):  # alpha NaN
         _lib.check(L.tmfwm_embed(p(a), 1, 16, 16, a.size, p(t), 8, float("nan"), p(o), _lib.MEM_HOST, None), "embed")
     assert "frame_stride" in _lib.last_error() or "alpha" in _lib.last_error()
-    for bad_route in (-1, 3):  # TMFWM_ROUTE_HYBRID / _REFERENCE / _RANK1 only
+    for bad_route in (-1, 4):  # TMFWM_ROUTE_HYBRID / _REFERENCE / _RANK1 / _RANK1_REFERENCE only
         with pytest.raises(ValueError, match="route"):
             _lib.check(L.tmfwm_embed_route(p(a), 1, 16, 16, a.size, p(t), 8, 0.1, p(o), _lib.MEM_HOST, None, bad_route, None), "e")
         with pytest.raises(ValueError, match="route"):
@@ -132,7 +132,7 @@ def test_multi_entry_points_validate_then_need_a_device():
         multi.embed_multi(a, t, 8, 0.1, route="exact")
     with pytest.raises(ValueError, match="route"):
         _lib.check(_lib.load().tmfwm_embed_multi_route(a.ctypes.data, 2, 16, 16, 16 * 16 * 3, t.ctypes.data, 8, 0.1, a.ctypes.data,
-                                                       None, 0, 3, None), "embed_multi_route")
+                                                       None, 0, 4, None), "embed_multi_route")
     with pytest.raises(ValueError):  # alpha = 0 divides by zero in extract (watermarking.py:285)
         _lib.check(L.tmfwm_extract_multi(p(a), p(a), 2, 16, 16, 16 * 16 * 3, 8, 0.0, p(t), None, 0, None), "extract_multi")
     if _lib.device_count() == 0:

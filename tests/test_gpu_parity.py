@@ -939,9 +939,9 @@ def test_hybrid_vs_reference_route_alpha_edges(dev, b):
 @pytest.mark.parametrize("b", [8, 16])
 @pytest.mark.parametrize("wm", ["noise", "qr"])
 def test_rank1_route_equals_reference_route_4k(dev, wm, b):
-    """TMFWM_ROUTE_RANK1 (ABI 10): the rank-1 pre-pass keeps the bytes of the blocks
+    """TMFWM_ROUTE_RANK1 / _RANK1_REFERENCE (ABI 10): the rank-1 pre-pass keeps the bytes of the blocks
     whose f32(D + c u1 v1^T) it proves equal to the reference's and sends the rest through the
-    hybrid route.  Its bytes equal the reference route's (np.linalg.svd's arithmetic on every
+    hybrid route (rank1) or straight to the dgesdd route (rank1_reference).  Its bytes equal the reference route's (np.linalg.svd's arithmetic on every
     block) on camera-like 4K covers, where it decides most blocks itself under a continuous
     watermark (under a binary one the w = 0 blocks sit on truncation boundaries and go to the list
     pass), and on the bench's noise covers, where most go to the list pass."""
@@ -967,6 +967,14 @@ def test_rank1_route_equals_reference_route_4k(dev, wm, b):
         total = n * (H // b) * (W // b)
         if kind == "photo" and wm == "noise":
             assert st["list_pass_blocks"] < total // 2, st  # the pre-pass decided most blocks itself
+        # the same pre-pass in front of the dgesdd route (no Jacobi SVD), and its extract
+        st2 = {}
+        o2 = batch.embed_batch(fr, tile, b, 0.1, route="rank1_reference", stats=st2)
+        assert torch.equal(o2, orf), (kind, blocks_differing(o2, orf, b), st2)
+        if kind == "photo" and wm == "noise":
+            assert st2["lapack_blocks"] < total // 2, st2
+        assert torch.equal(batch.extract_batch(orf, fr, b, 0.1, route="rank1_reference"),
+                           batch.extract_batch(orf, fr, b, 0.1, route="reference"))
 
 
 def test_rank1_route_edges(dev):
@@ -989,9 +997,10 @@ def test_rank1_route_edges(dev):
     for b in (8, 12, 16):
         tile = torch.from_numpy(_u8(93 + b, (H // b, W // b)) & np.uint8(1)).to(dev) * 255
         for alpha in (0.1, 0.0, 1.0, -0.05, -5.0):
-            o1 = batch.embed_batch(fr, tile, b, alpha, route="rank1")
             orf = batch.embed_batch(fr, tile, b, alpha, route="reference")
-            assert torch.equal(o1, orf), (b, alpha)
+            for rt in ("rank1", "rank1_reference"):
+                o1 = batch.embed_batch(fr, tile, b, alpha, route=rt)
+                assert torch.equal(o1, orf), (b, alpha, rt)
 
 
 @pytest.mark.parametrize("mem", ["host", "device"])

@@ -29,7 +29,8 @@ ERR_NODATA = -61
 ROUTE_HYBRID = 0  # TMFWM_ROUTE_*: the SVD route of embed / extract (include/tmfwm.h)
 ROUTE_REFERENCE = 1
 ROUTE_RANK1 = 2  # ABI 10: the hybrid route behind the rank-1 pre-pass (embed at b = 8, 16; photo mode)
-ROUTES = {"hybrid": ROUTE_HYBRID, "reference": ROUTE_REFERENCE, "rank1": ROUTE_RANK1}
+ROUTE_RANK1_REFERENCE = 3  # ABI 10: the rank-1 pre-pass in front of the dgesdd route (no Jacobi, no K)
+ROUTES = {"hybrid": ROUTE_HYBRID, "reference": ROUTE_REFERENCE, "rank1": ROUTE_RANK1, "rank1_reference": ROUTE_RANK1_REFERENCE}
 
 # pixel layouts of tmfwm_embed_px / tmfwm_extract_px (include/tmfwm.h, ABI 8)
 PIX_RGB = 3
@@ -37,12 +38,12 @@ PIX_RGBX = 4  # PIL's in-memory mode "RGB" (R, G, B, pad)
 
 
 def route_code(route) -> int:
-    """"hybrid" / "reference" / "rank1" (or the TMFWM_ROUTE_* value) -> the ABI's route value."""
+    """"hybrid" / "reference" / "rank1" / "rank1_reference" (or the TMFWM_ROUTE_* value) -> the ABI's route value."""
     if isinstance(route, str):
         if route not in ROUTES:
             raise ValueError(f"route must be one of {sorted(ROUTES)}, got {route!r}")
         return ROUTES[route]
-    if route not in (ROUTE_HYBRID, ROUTE_REFERENCE, ROUTE_RANK1):
+    if route not in (ROUTE_HYBRID, ROUTE_REFERENCE, ROUTE_RANK1, ROUTE_RANK1_REFERENCE):
         raise ValueError(f"route {route!r}")
     return int(route)
 

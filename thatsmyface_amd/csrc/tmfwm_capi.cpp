@@ -294,7 +294,8 @@ int run_embed(EmbedArgs a, hipStream_t st, int64_t *n_lapack, bool check, uint32
     DevBuf list, slow, shards, counts;
     if (ch.cap > 0) {
         if (int rc = list.alloc((size_t)ch.cap * 4, st, "dgesdd-route block list")) return rc;
-        if ((embed_defers(a.block) && route != TMFWM_ROUTE_REFERENCE) || (route == TMFWM_ROUTE_RANK1 && rank1_block(a.block))) {
+        if ((embed_defers(a.block) && route != TMFWM_ROUTE_REFERENCE && route != TMFWM_ROUTE_RANK1_REFERENCE) ||
+            (route == TMFWM_ROUTE_RANK1 && rank1_block(a.block))) {
             if (int rc = slow.alloc((size_t)ch.cap * 4, st, "list-pass block list")) return rc;
             if (int rc = shards.alloc((size_t)kListShards * kShardStride * 4, st, "list-pass segment counters")) return rc;
         }
@@ -324,10 +325,13 @@ int run_embed(EmbedArgs a, hipStream_t st, int64_t *n_lapack, bool check, uint32
         k.slow_count = static_cast<uint32_t *>(counts.p) + 2 * ch.n + c;
         k.slow_shards = static_cast<uint32_t *>(shards.p);
         if (shards.p) TMF_HIP(hipMemsetAsync(shards.p, 0, (size_t)kListShards * kShardStride * 4, st));
-        if (route == TMFWM_ROUTE_REFERENCE) {  // every block on the dgesdd route; the edges as always
+        const bool pre = (route == TMFWM_ROUTE_RANK1 || route == TMFWM_ROUTE_RANK1_REFERENCE) && rank1_block(k.block);
+        if (route == TMFWM_ROUTE_REFERENCE || (route == TMFWM_ROUTE_RANK1_REFERENCE && !pre)) {
+            // every block on the dgesdd route; the edges as always
             TMF_HIP(launch_edges(k.src, k.dst, k.nframes, k.H, k.W, k.frame_stride, k.block, st));
             TMF_HIP(launch_list_all(k.fb_list, k.fb_count, k.nframes * ch.per_frame, st));
-        } else if (route == TMFWM_ROUTE_RANK1) {  // the rank-1 pre-pass, its list pass, the edges
+        } else if (pre) {  // the rank-1 pre-pass (+ its list pass for TMFWM_ROUTE_RANK1), the edges
+            if (route == TMFWM_ROUTE_RANK1_REFERENCE) k.slow_list = nullptr;
             TMF_HIP(launch_embed_rank1(k, st));
         } else {
             TMF_HIP(launch_embed(k, st));
@@ -491,7 +495,7 @@ int tmfwm_embed_route(const uint8_t *rgb, int64_t n_frames, int32_t height, int3
                       int32_t route, int64_t *n_lapack_blocks)
 {
     t_err.clear();
-    if (route != TMFWM_ROUTE_HYBRID && route != TMFWM_ROUTE_REFERENCE && route != TMFWM_ROUTE_RANK1) return fail(TMFWM_ERR_INVALID, "route %d", route);
+    if (route < TMFWM_ROUTE_HYBRID || route > TMFWM_ROUTE_RANK1_REFERENCE) return fail(TMFWM_ERR_INVALID, "route %d", route);
     if (n_lapack_blocks) {
         *n_lapack_blocks = 0;
         t_list_pass = 0;  // this call's count from here on (an early return leaves 0)
@@ -564,7 +568,7 @@ int tmfwm_extract_route(const uint8_t *wm_rgb, const uint8_t *orig_rgb, int64_t 
                         void *hip_stream, int32_t route, int64_t *n_lapack_blocks)
 {
     t_err.clear();
-    if (route != TMFWM_ROUTE_HYBRID && route != TMFWM_ROUTE_REFERENCE && route != TMFWM_ROUTE_RANK1) return fail(TMFWM_ERR_INVALID, "route %d", route);
+    if (route < TMFWM_ROUTE_HYBRID || route > TMFWM_ROUTE_RANK1_REFERENCE) return fail(TMFWM_ERR_INVALID, "route %d", route);
     if (n_lapack_blocks) {
         *n_lapack_blocks = 0;
         t_list_pass = 0;  // this call's count from here on (an early return leaves 0)
@@ -678,7 +682,7 @@ int tmfwm_embed_px(const uint8_t *rgb, int32_t in_pixel_bytes, int64_t in_frame_
         return tmfwm_embed_route(rgb, n_frames, height, width, in_frame_stride, wm_tile, block, alpha, out, mem_kind, hip_stream,
                                  route, n_lapack_blocks);
     }
-    if (route != TMFWM_ROUTE_HYBRID && route != TMFWM_ROUTE_REFERENCE && route != TMFWM_ROUTE_RANK1) return fail(TMFWM_ERR_INVALID, "route %d", route);
+    if (route < TMFWM_ROUTE_HYBRID || route > TMFWM_ROUTE_RANK1_REFERENCE) return fail(TMFWM_ERR_INVALID, "route %d", route);
     if (n_lapack_blocks) {
         *n_lapack_blocks = 0;
         t_list_pass = 0;
@@ -757,7 +761,7 @@ int tmfwm_extract_px(const uint8_t *wm_rgb, int32_t wm_pixel_bytes, int64_t wm_f
     if (wm_pixel_bytes == TMFWM_PIX_RGB && orig_pixel_bytes == TMFWM_PIX_RGB && wm_frame_stride == orig_frame_stride)
         return tmfwm_extract_route(wm_rgb, orig_rgb, n_frames, height, width, wm_frame_stride, block, alpha, out_tiles, mem_kind,
                                    hip_stream, route, n_lapack_blocks);
-    if (route != TMFWM_ROUTE_HYBRID && route != TMFWM_ROUTE_REFERENCE && route != TMFWM_ROUTE_RANK1) return fail(TMFWM_ERR_INVALID, "route %d", route);
+    if (route < TMFWM_ROUTE_HYBRID || route > TMFWM_ROUTE_RANK1_REFERENCE) return fail(TMFWM_ERR_INVALID, "route %d", route);
     if (n_lapack_blocks) {
         *n_lapack_blocks = 0;
         t_list_pass = 0;

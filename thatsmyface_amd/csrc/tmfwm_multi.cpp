@@ -457,7 +457,7 @@ int tmfwm_embed_multi_route(const uint8_t *rgb, int64_t n_frames, int32_t height
 {
     tmf::clear_error();
     if (n_lapack_blocks) *n_lapack_blocks = 0;
-    if (route != TMFWM_ROUTE_HYBRID && route != TMFWM_ROUTE_REFERENCE && route != TMFWM_ROUTE_RANK1) return report(TMFWM_ERR_INVALID, "route %d", route);
+    if (route < TMFWM_ROUTE_HYBRID || route > TMFWM_ROUTE_RANK1_REFERENCE) return report(TMFWM_ERR_INVALID, "route %d", route);
     if (int rc = tmf::check_frames(n_frames, height, width, frame_stride, block)) return rc;
     if (!std::isfinite(alpha)) return report(TMFWM_ERR_INVALID, "alpha is not finite");
     const int nbh = height / block, nbw = width / block;
@@ -513,7 +513,7 @@ int tmfwm_extract_multi_route(const uint8_t *wm_rgb, const uint8_t *orig_rgb, in
 {
     tmf::clear_error();
     if (n_lapack_blocks) *n_lapack_blocks = 0;
-    if (route != TMFWM_ROUTE_HYBRID && route != TMFWM_ROUTE_REFERENCE && route != TMFWM_ROUTE_RANK1) return report(TMFWM_ERR_INVALID, "route %d", route);
+    if (route < TMFWM_ROUTE_HYBRID || route > TMFWM_ROUTE_RANK1_REFERENCE) return report(TMFWM_ERR_INVALID, "route %d", route);
     if (int rc = tmf::check_frames(n_frames, height, width, frame_stride, block)) return rc;
     if (!std::isfinite(alpha) || alpha == 0.0) return report(TMFWM_ERR_INVALID, "alpha must be finite and non-zero");
     const int64_t tbytes = (int64_t)(height / block) * (width / block);

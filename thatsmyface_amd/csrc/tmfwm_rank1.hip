@@ -22,9 +22,11 @@
 // |r| / (|v| gap); u = D v / |D v| is no further from u1; LAPACK's own top pair is within
 // 1024 2^-53 s1 / (s1 - s2) (ten times the worst any triplet showed in the K study, 3.5; the
 // pass requires e <= 2^-30, so e's share of the bound is below 2^-29 |c| whatever that constant).
-// A block that fails any test (gap <= 0, e > 2^-30, an undecided byte) writes nothing and goes to
-// the slow list; the list pass (embed_kernel<b, true>) redoes it on the full hybrid route --
-// Jacobi SVD, byte certificate, dgesdd route -- so every byte is the reference's either way.
+// A block that fails any test (no spectral gap, an undecided byte) writes nothing and goes to the
+// slow list, whose list pass (embed_kernel<b, true>) redoes it on the full hybrid route -- Jacobi
+// SVD, byte certificate, dgesdd route (TMFWM_ROUTE_RANK1) -- or straight to the dgesdd route
+// (TMFWM_ROUTE_RANK1_REFERENCE, no Jacobi factors and so no K), so every byte is the reference's
+// either way.
 #include "tmfwm_blocks.h"
 
 namespace tmf {
@@ -308,10 +310,14 @@ __global__ __launch_bounds__(64, B == 8 ? 3 : 2) void embed_rank1_kernel(EmbedAr
             uint8_t *pp = dst + ((int64_t)(pos.bi * B + q * R + r) * a.W + (int64_t)pos.bj * B) * 3;
             if (real_row<B>(q, r)) store_words<B>(pp, a.aligned, outw[r]);
         }
-    } else if (q == 0) {  // the full hybrid route in the list pass
-        const uint32_t row = blockIdx.y * (uint32_t)a.nbh + (uint32_t)pos.bi, s = row % kListShards;
-        a.slow_list[shard_base(s, (uint32_t)a.nframes * (uint32_t)a.nbh, (uint32_t)a.nbw) +
-                    atomicAdd(a.slow_shards + s * kShardStride, 1u)] = id;
+    } else if (q == 0) {
+        if (a.slow_list) {  // TMFWM_ROUTE_RANK1: the full hybrid route in the list pass
+            const uint32_t row = blockIdx.y * (uint32_t)a.nbh + (uint32_t)pos.bi, s = row % kListShards;
+            a.slow_list[shard_base(s, (uint32_t)a.nframes * (uint32_t)a.nbh, (uint32_t)a.nbw) +
+                        atomicAdd(a.slow_shards + s * kShardStride, 1u)] = id;
+        } else {  // TMFWM_ROUTE_RANK1_REFERENCE: the dgesdd route (embed_fixup_kernel)
+            a.fb_list[atomicAdd(a.fb_count, 1u)] = id;
+        }
     }
 }
 
@@ -327,20 +333,23 @@ static hipError_t launch_rank1_b(EmbedArgs a, hipStream_t st)
         c.dst = a.dst + f0 * a.frame_stride;
         hipLaunchKernelGGL((embed_rank1_kernel<B>), dim3((unsigned)gx, (unsigned)nf), dim3(64), 0, st, c);
     }
-    const int64_t rows = a.nframes * a.nbh;
-    const unsigned grid = (unsigned)(rows < (int64_t)kListShards ? rows : (int64_t)kListShards);
-    hipLaunchKernelGGL((embed_kernel<B, true>), dim3(grid), dim3(64), 0, st, a);
+    if (a.slow_list) {  // TMFWM_ROUTE_RANK1: the list pass over the blocks the pre-pass left
+        const int64_t rows = a.nframes * a.nbh;
+        const unsigned grid = (unsigned)(rows < (int64_t)kListShards ? rows : (int64_t)kListShards);
+        hipLaunchKernelGGL((embed_kernel<B, true>), dim3(grid), dim3(64), 0, st, a);
+    }
     return hipGetLastError();
 }
 
 bool rank1_block(int block) { return block == 8 || block == 16; }
 
-// TMFWM_ROUTE_RANK1 at b = 8 / 16: the pre-pass over every block, the list pass (embed_kernel<b,
-// true>: the full hybrid route) over the blocks it left, the edge pixels; the caller runs the
-// dgesdd-route fixup as for the hybrid route.  Other block sizes: the hybrid route.
+// The rank-1 pre-pass at b = 8 / 16 over every block, then the edge pixels.  TMFWM_ROUTE_RANK1
+// (a.slow_list set): the list pass (embed_kernel<b, true>: the full hybrid route) over the blocks
+// it left; TMFWM_ROUTE_RANK1_REFERENCE (no slow list): those blocks went to the dgesdd-route list.
+// Either way the caller runs the dgesdd-route fixup next.  The caller handles other block sizes.
 hipError_t launch_embed_rank1(EmbedArgs a, hipStream_t st)
 {
-    if (!rank1_block(a.block) || !a.slow_list) return launch_embed(a, st);
+    if (!rank1_block(a.block)) return hipErrorInvalidValue;
     if (a.nbh > 0 && a.nbw > 0) {
         const hipError_t e = a.block == 8 ? launch_rank1_b<8>(a, st) : launch_rank1_b<16>(a, st);
         if (e != hipSuccess) return e;

@@ -58,6 +58,12 @@ def main():
     rs = dict(cs, svd_route="reference")
     out["embed_watermark_reference_route_ms"] = timed(lambda: W.embed_watermark(cover, png, True, rs))
     out["extract_watermark_reference_route_ms"] = timed(lambda: W.extract_watermark(wm_img, cover, rs))
+    r1 = dict(cs, svd_route="rank1_reference")  # round 6: the rank-1 pre-pass in front of the dgesdd route
+    out["embed_watermark_rank1_reference_route_ms"] = timed(lambda: W.embed_watermark(cover, png, True, r1))
+    out["extract_watermark_rank1_reference_route_ms"] = timed(lambda: W.extract_watermark(wm_img, cover, r1))
+    r2 = dict(cs, svd_route="hybrid")
+    out["embed_watermark_hybrid_route_ms"] = timed(lambda: W.embed_watermark(cover, png, True, r2))
+    out["extract_watermark_hybrid_route_ms"] = timed(lambda: W.extract_watermark(wm_img, cover, r2))
     # the extract page's inputs are decoded uploads, not embed_watermark's own output image
     b2 = io.BytesIO()
     wm_img.save(b2, format="PNG")

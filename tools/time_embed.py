@@ -24,7 +24,7 @@ def main():
     p.add_argument("--reps", type=int, default=3)
     p.add_argument("--kind", choices=["noise", "photo"], default="noise", help="covers: the bench's noise or camera-like")
     p.add_argument("--wm", choices=["noise", "qr"], default="noise", help="watermark tile: uniform bytes or binary (QR)")
-    p.add_argument("--route", choices=["hybrid", "reference", "rank1"], default="hybrid")
+    p.add_argument("--route", choices=["hybrid", "reference", "rank1", "rank1_reference"], default="hybrid")
     p.add_argument("--hash", action="store_true", help="sha256 of the embed output and the extracted tiles (A/B identity)")
     a = p.parse_args()
     dev = torch.device("cuda", 0)
