@@ -49,3 +49,22 @@ def test_fast_path_certificate_is_sound():
         assert r["certified_blocks_differing_from_lapack"] == 0, (k, r)
     assert res["noise"]["frac_exact_path"] > 0.4
     assert res["photo"]["frac_exact_path"] < 0.3
+
+
+@pytest.mark.parametrize("b", [8, 16])
+def test_rank1_prepass_bound_is_sound(b):
+    """The shipped rank-1 pre-pass's bound (csrc/tmfwm_rank1.hip) restated in numpy
+    (fastpath_study.certify_rank1): every block it decides has the dgesdd route's bytes, with the
+    noise and a binary (0 / 255) watermark; it decides most camera-like blocks under the noise
+    watermark and few noise-cover blocks."""
+    import fastpath_study as F
+
+    H, W = 272, 480
+    covs = _covers(H, W, 13)
+    tn = O.synth_bytes(0x5EED0002, 13, 1, (H // b) * (W // b)).reshape(H // b, W // b)
+    for wm, tile in (("noise", tn), ("qr", (tn & 1) * 255)):
+        res = {k: F.certify_rank1(c, tile, b) for k, c in covs.items()}
+        for k, r in res.items():
+            assert r["decided_blocks_differing"] == 0, (wm, k, r)
+        if wm == "noise":
+            assert res["photo"]["undecided"] < 0.35 and res["noise"]["undecided"] > 0.4, res

@@ -109,6 +109,82 @@ def certify(cov, tile, b, alpha=0.1, K_A=1024.0, K_uv=1024.0, kappa=2.0, L=16, r
     return res
 
 
+def certify_rank1(cov, tile, b, alpha=0.1, iters=4):
+    """The shipped pre-pass's bound (csrc/tmfwm_rank1.hip, round 6) restated in numpy: the top
+    pair from `iters` f64 power steps on D^T D from the column-norm vector with the a-posteriori
+    angle (Kato-Temple margins, Davis-Kahan) plus LAPACK's 1024 2^-53 s1 / (s1 - s2); dM in rank-one
+    form (alpha' G + beta' P + gamma'); the IDCT roundings through |M_fast| <= G + |c| P; bytes at
+    both ends of [Y_fast - eps_Y, Y_fast + eps_Y].  Returns the undecided fraction and the number of
+    decided blocks whose bytes differ from the dgesdd route's (the soundness check)."""
+    H, W = cov.shape[:2]
+    nbh, nbw = H // b, W // b
+    ycc = O.rgb_to_ycbcr(cov)
+    D = O.dct2d_blocks(_blocks(ycc[..., 0], b))
+    D64 = D.astype(np.float64)
+    n = len(D)
+    rn = (D64**2).sum(axis=2)
+    cn = (D64**2).sum(axis=1)
+    F = cn.sum(axis=1)
+    zero = F == 0
+    v = np.where(zero[:, None], np.eye(b)[0][None, :], cn)
+    for _ in range(iters):
+        w = np.einsum("nij,ni->nj", D64, np.einsum("nij,nj->ni", D64, v))
+        nn = (w**2).sum(axis=1)
+        live = (nn > 0)[:, None]
+        v = np.where(live, w / np.sqrt(np.where(live[:, 0], nn, 1.0))[:, None], v)
+    nv = (v**2).sum(axis=1)
+    t = np.einsum("nij,nj->ni", D64, v)
+    tt = (t**2).sum(axis=1)
+    rho = tt / np.where(nv > 0, nv, 1)
+    r = np.einsum("nij,ni->nj", D64, t) - rho[:, None] * v
+    rr0 = np.sqrt((r**2).sum(axis=1) / np.where(nv > 0, nv, 1)) * (1 + 16 * EPS) + 256 * EPS * F
+    rlo, fhi = rho * (1 - 256 * EPS), F * (1 + 256 * EPS)
+    gap = 2 * rlo - fhi
+    lhi = (rho + rr0**2 / np.where(gap > 0, gap, 1)) * (1 + 256 * EPS)
+    s1hi = np.sqrt(lhi) * (1 + 512 * EPS)
+    s2hi = np.sqrt(np.maximum(fhi - rlo, 0)) * (1 + 512 * EPS)
+    g1 = np.sqrt(rlo) * (1 - 512 * EPS) - s2hi
+    e = np.where(zero, 0.0, 1.01 * rr0 / np.where(gap > 0, gap, 1) + 1024 * EPS * s1hi / np.where(g1 > 0, g1, 1) + 2.0**-45)
+    ok = zero | ((gap > 0) & (g1 > 0))
+    u = np.where(zero[:, None], np.eye(b)[0][None, :], t / np.sqrt(np.where(tt > 0, tt, 1))[:, None])
+    v = v / np.sqrt(np.where(nv > 0, nv, 1))[:, None]
+    c = alpha * (tile.reshape(-1).astype(np.float64) / 255.0)
+    Mf = (D64 + c[:, None, None] * u[:, :, None] * v[:, None, :]).astype(np.float32)
+    Yf = O.dct2d_blocks(Mf, inverse=True)
+    ca = np.abs(c)
+    al = 1.01 * (b + 6) * U32
+    be = 1.01 * ((b + 6) * U32 * ca + 2 * U32 * (s1hi + ca))
+    ga = 2.0**-40 * s1hi + ca * e * (2 + e)
+    gL = 16 * U32 / (1 - 16 * U32)
+    k1, k2, k3 = 2 * (al * (1 + 2 * gL) + 2 * gL), 2 * (be * (1 + 2 * gL) + 2 * gL * ca), 2 * ga * (1 + 2 * gL)
+    k1 = np.broadcast_to(np.asarray(k1, np.float64), (n,))
+    C = np.abs(dct_matrix(b)).T  # the IDCT matrix |C|[p][i]
+    a_ = np.sqrt(np.sqrt(rn))
+    b_ = np.sqrt(np.sqrt(cn))
+    up, vp = np.abs(u) + e[:, None], np.abs(v) + e[:, None]
+    A, Bq = a_ @ C.T, b_ @ C.T
+    Up, Vq = up @ C.T, vp @ C.T
+    S = C.sum(axis=1)
+    epsY = (k1[:, None, None] * A[:, :, None] * Bq[:, None, :] + k2[:, None, None] * Up[:, :, None] * Vq[:, None, :]
+            + k3[:, None, None] * S[None, :, None] * S[None, None, :]) * (1 + 2.0**-16) + np.abs(Yf) * 2.0**-22 + 2.0**-40
+    Yp = _unblocks(Yf, nbh, nbw, b).astype(np.float64)
+    Ep = _unblocks(epsY, nbh, nbw, b)
+    cbp = (ycc[: nbh * b, : nbw * b, 1] - np.float32(0.5)).astype(np.float64)
+    crp = (ycc[: nbh * b, : nbw * b, 2] - np.float32(0.5)).astype(np.float64)
+    okp = np.ones(Yp.shape, bool)
+    for a_cr, a_cb in ((1.403, 0.0), (-0.714, -0.344), (0.0, 1.773)):
+        tcol = Yp + a_cr * crp + a_cb * cbp
+        slack = Ep + 2 * U32 * np.abs(tcol) + 1e-12
+        okp &= byte_of(tcol - slack) == byte_of(tcol + slack)
+    cert = okp.reshape(nbh, b, nbw, b).all(axis=(1, 3)).reshape(-1) & ok
+    out_fast = ycc.copy()
+    out_fast[: nbh * b, : nbw * b, 0] = _unblocks(Yf, nbh, nbw, b)
+    fast = O.ycbcr_to_rgb(out_fast)
+    ref = O.embed_frame(cov, tile, b, alpha, route="lapack")
+    bd = (fast != ref)[: nbh * b, : nbw * b].reshape(nbh, b, nbw, b, 3).any(axis=(1, 3, 4)).reshape(-1)
+    return {"blocks": n, "undecided": float(1 - cert.mean()), "decided_blocks_differing": int((bd & cert).sum())}
+
+
 def main():
     b, nfr = int(sys.argv[1]), int(sys.argv[2])
     H, W = (int(x) for x in sys.argv[3:5]) if len(sys.argv) > 4 else (2160, 3840)
