@@ -69,10 +69,11 @@ def parse(argv=None):
                         "a differing byte fails the run (exit status 3)")
     p.add_argument("--pg-timeout", type=float, default=600.0,
                    help="seconds a rank may wait in a collective before the run fails (N > 1)")
-    p.add_argument("--route", default="hybrid", choices=["hybrid", "reference", "rank1"],
+    p.add_argument("--route", default="hybrid", choices=["hybrid", "reference", "rank1", "rank1_reference"],
                    help="SVD route (DESIGN.md 3.5): hybrid = Jacobi + byte certificate (the throughput route); "
                         "reference = the dgesdd route for every block (np.linalg.svd's arithmetic by construction); "
-                        "rank1 = the hybrid route behind the rank-1 pre-pass (b = 8, photo mode, DESIGN.md 5)")
+                        "rank1 = the hybrid route behind the rank-1 pre-pass (b = 8 / 16, photo mode, DESIGN.md 5); "
+                        "rank1_reference = the reference route behind it")
     p.add_argument("--covers", default="noise", choices=["noise", "photo"],
                    help="synthetic covers: uniform bytes (configs[1]-[4], the default) or camera-like frames")
     p.add_argument("--wm", default="noise", choices=["noise", "qr"],
@@ -580,8 +581,10 @@ def run(args, kernels=None, device=None):
         return None
 
     # HBM bytes of the embed launch: counted FETCH / WRITE bytes per frame x frames
+    # (hybrid route only: the other routes launch other kernels)
+    route = getattr(K, "route", "hybrid")
     traffic = None
-    ek = profiled(f"embed_kernel<{b}>")
+    ek = profiled(f"embed_kernel<{b}>") if route == "hybrid" else None
     if ek and ek.get("hbm_bytes_per_frame"):
         traffic = int(ek["hbm_bytes_per_frame"] * F)
 
@@ -590,7 +593,7 @@ def run(args, kernels=None, device=None):
     # peak VALU issue
     valu = {}
     for name, ms in ((f"embed_kernel<{b}>", embed_ms), (f"extract_kernel<{b}>", extract_ms)):
-        k = profiled(name)
+        k = profiled(name) if route == "hybrid" or name.startswith("extract") and route != "reference" else None
         if k and k.get("clock_MHz"):
             got = ms * 1e3 / F
             frac = k["issue_bound_cycles_per_frame"] / (got * k["clock_MHz"])
@@ -633,11 +636,17 @@ def run(args, kernels=None, device=None):
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": f"embed_kernel<{b}>",
-                "launch": (f"one tmfwm_embed call: embed_kernel<{b}> strip pass"
-                           + (" + list pass" if getattr(K, "embed_list_pass", lambda _b: False)(b) else "")
-                           + f" + embed_fixup_kernel<{b}> (dgesdd route)") if getattr(K, "route", "hybrid") == "hybrid" else
-                          f"one tmfwm_embed_route call, TMFWM_ROUTE_REFERENCE: embed_fixup_kernel<{b}> (dgesdd route) on every block",
+                "kernel": {"reference": f"embed_fixup_kernel<{b}>"}.get(route, f"embed_rank1_kernel<{b}>" if route.startswith("rank1") else f"embed_kernel<{b}>"),
+                "launch": {
+                    "hybrid": (f"one tmfwm_embed call: embed_kernel<{b}> strip pass"
+                               + (" + list pass" if getattr(K, "embed_list_pass", lambda _b: False)(b) else "")
+                               + f" + embed_fixup_kernel<{b}> (dgesdd route)"),
+                    "reference": f"one tmfwm_embed_route call, TMFWM_ROUTE_REFERENCE: embed_fixup_kernel<{b}> (dgesdd route) on every block",
+                    "rank1": (f"one tmfwm_embed_route call, TMFWM_ROUTE_RANK1: embed_rank1_kernel<{b}> (rank-1 pre-pass) + "
+                              f"embed_kernel<{b}> list pass (hybrid route) + embed_fixup_kernel<{b}> (dgesdd route)"),
+                    "rank1_reference": (f"one tmfwm_embed_route call, TMFWM_ROUTE_RANK1_REFERENCE: embed_rank1_kernel<{b}> "
+                                        f"(rank-1 pre-pass) + embed_fixup_kernel<{b}> (dgesdd route) on the blocks it leaves"),
+                }[route],
                 "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
