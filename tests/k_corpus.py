@@ -82,6 +82,41 @@ def ratios(D: np.ndarray):
     return cert, ru, rv, rs
 
 
+# The rank-1 pre-pass's LAPACK constants (csrc/tmfwm_rank1.hip: gamma' = 2^-40 s1, the top pair
+# within 1024 2^-53 s1 / (s1 - s2)), measured by tools/exp/lapack_bounds.py
+RESID_UNITS = 8192
+PAIR_UNITS = 1024
+
+
+def residual_units(D, U, S, V):
+    """max_ij |(U S V^T)_ij - D_ij| / (2^-53 sigma_1) per block, in extended precision."""
+    Ul, Sl, Vl = (x.astype(np.longdouble) for x in (U, S, V))
+    M = np.einsum("nik,nk,njk->nij", Ul, Sl, Vl)
+    r = np.abs(M - D.astype(np.longdouble)).reshape(len(D), -1).max(axis=1).astype(np.float64)
+    s1 = S.max(axis=1)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        return np.where(s1 > 0, r / (EPS * s1), 0.0)
+
+
+def top_pair_units(D, S_l, U_l, V_l):
+    """max |F_J - F_L| over the top triplet's elements, units 2^-53 s1 / (s1 - s2)."""
+    Uj, sj, Vj = O.svd_blocks_f64(D)
+    n = len(D)
+    kj = np.argmax(sj, axis=1)
+    kl = np.argmax(S_l, axis=1)
+    uj, vj = Uj[np.arange(n), :, kj], Vj[np.arange(n), :, kj]
+    ul, vl = U_l[np.arange(n), :, kl], V_l[np.arange(n), :, kl]
+    sg = np.sign(np.einsum("nr,nr->n", uj, ul))
+    sg[sg == 0] = 1
+    d = np.maximum(np.abs(uj - ul * sg[:, None]).max(axis=1), np.abs(vj - vl * sg[:, None]).max(axis=1))
+    s = np.sort(sj, axis=1)
+    s1, s2 = s[:, -1], s[:, -2]
+    ok = s1 > s2
+    with np.errstate(divide="ignore", invalid="ignore"):
+        return ok, np.where(ok, d / (EPS * s1 / np.where(ok, s1 - s2, 1.0)), 0.0)
+
+
+
 # ---- cover classes ----------------------------------------------------------------------
 
 def _rand_orth(rng, n, b):
