@@ -53,16 +53,16 @@ extern "C" {
                                    prove (the throughput route: tmfwm_embed) */
 #define TMFWM_ROUTE_REFERENCE 1 /* the dgesdd route -- np.linalg.svd's own arithmetic -- for every
                                    block: the reference's bytes by construction */
-#define TMFWM_ROUTE_RANK1 2     /* (ABI 10) embed at b = 8 and 16: a rank-1 pre-pass keeps the bytes of every
+#define TMFWM_ROUTE_RANK1 2     /* (ABI 10) embed: a rank-1 pre-pass keeps the bytes of every
                                    block whose f32(D + c u1 v1^T) it proves equal to the reference's
                                    (photo mode) and sends the rest through the hybrid
-                                   route; other block sizes and extract: TMFWM_ROUTE_HYBRID */
+                                   route (every slider size, b = 4..16 even); extract:
+                                   TMFWM_ROUTE_HYBRID */
 #define TMFWM_ROUTE_RANK1_REFERENCE 3 /* (ABI 10) the same pre-pass in front of the dgesdd route: no
                                    Jacobi SVD and so no K -- embed rests on the pre-pass's rank-one
                                    bound (its constants on LAPACK's residual and top pair enter
                                    scaled by ~2^-24), extract on the certified sigma_1 enclosure
-                                   (TMFWM_ROUTE_HYBRID's extract); other block sizes: the dgesdd
-                                   route for every block */
+                                   (TMFWM_ROUTE_HYBRID's extract); every slider size */
 
 #define TMFWM_OK 0
 #define TMFWM_ERR_INVALID (-22)     /* bad argument (EINVAL) */
@@ -127,7 +127,7 @@ int tmfwm_embed_ex(const uint8_t *rgb, int64_t n_frames, int32_t height, int32_t
  * on (the hybrid route's bytes equal it through its byte certificate, which rests on one
  * measured bound).  About two orders of magnitude less
  * throughput than the hybrid route; *n_lapack_blocks then counts every block.
- * TMFWM_ROUTE_RANK1 (ABI 10): the hybrid route behind a rank-1 pre-pass (b = 8, 16; photographs,
+ * TMFWM_ROUTE_RANK1 (ABI 10): the hybrid route behind a rank-1 pre-pass (b = 4..16; photographs,
  * whose blocks it mostly decides alone); tmfwm_last_list_pass_blocks() then counts the blocks
  * it left to the hybrid route.
  */

@@ -977,11 +977,43 @@ def test_rank1_route_equals_reference_route_4k(dev, wm, b):
                            batch.extract_batch(orf, fr, b, 0.1, route="reference"))
 
 
+@pytest.mark.parametrize("b", [4, 6, 10, 12, 14])
+def test_rank1_route_other_slider_sizes(dev, b):
+    """The rank-1 pre-pass at the slider sizes other than 8 / 16 (IDCT tables of every length,
+    tools/exp/idct_bound.py): camera-like 1080p covers with a continuous and a binary watermark,
+    and a noise cover; both rank-1 routes equal the reference route byte for byte, and the pre-pass
+    decides most camera-like blocks itself under the continuous watermark."""
+    import sys as _sys
+
+    _sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "exp"))
+    from route_diff_gpu import photo_covers
+
+    from thatsmyface_amd import batch
+
+    H, W = 1080, 1920
+    fr = photo_covers(4, H, W, 95, dev)
+    fr[3] = torch.from_numpy(_u8(96, (H, W, 3))).to(dev)
+    total = 3 * (H // b) * (W // b)
+    for wm in ("noise", "qr"):
+        tile = batch.synth_tile(H // b, W // b, device=dev)
+        if wm == "qr":
+            tile = (tile & 1) * 255
+        orf = batch.embed_batch(fr, tile, b, 0.1, route="reference")
+        for rt in ("rank1", "rank1_reference"):
+            st = {}
+            o = batch.embed_batch(fr[:3], tile, b, 0.1, route=rt, stats=st)
+            assert torch.equal(o, orf[:3]), (b, wm, rt, st)
+            if wm == "noise":
+                key = "list_pass_blocks" if rt == "rank1" else "lapack_blocks"
+                assert st[key] < total // 2, (b, rt, st)
+            assert torch.equal(batch.embed_batch(fr[3:], tile, b, 0.1, route=rt), orf[3:]), (b, wm, rt)
+
+
 def test_rank1_route_edges(dev):
     """The rank-1 pre-pass on its edge cases: zero (black) and flat frames (D = 0, D zero but for
     D[0][0]), frames whose size is not a multiple of b (edge pixels), alpha = 0, large and negative
-    alpha (S'[0] < 0), a frame of noise next to camera-like ones, at b = 8 and 16; other block sizes
-    take the hybrid route.  Every byte equals the reference route's."""
+    alpha (S'[0] < 0), a frame of noise next to camera-like ones, at every slider size.  Every byte
+    equals the reference route's."""
     import sys as _sys
 
     _sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "exp"))
@@ -994,7 +1026,7 @@ def test_rank1_route_edges(dev):
     fr[1] = 0
     fr[2] = torch.tensor([37, 140, 201], dtype=torch.uint8, device=dev)
     fr[3] = torch.from_numpy(_u8(92, (H, W, 3))).to(dev)
-    for b in (8, 12, 16):
+    for b in (4, 6, 8, 10, 12, 14, 16):
         tile = torch.from_numpy(_u8(93 + b, (H // b, W // b)) & np.uint8(1)).to(dev) * 255
         for alpha in (0.1, 0.0, 1.0, -0.05, -5.0):
             orf = batch.embed_batch(fr, tile, b, alpha, route="reference")

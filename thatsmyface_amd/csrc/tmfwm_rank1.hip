@@ -28,52 +28,19 @@
 // (TMFWM_ROUTE_RANK1_REFERENCE, no Jacobi factors and so no K), so every byte is the reference's
 // either way.
 #include "tmfwm_blocks.h"
+#include "tmfwm_idct_bounds.h"
 
 namespace tmf {
 
 extern template __global__ void embed_kernel<8, true>(EmbedArgs);  // tmfwm_embed8.hip
-// the list pass of b = 16 exists for this route only (the hybrid route's strip pass at b = 16 runs
-// every block to the end, kDeferMax<16> = 0): instantiated here
-template __global__ void embed_kernel<16, true>(EmbedArgs);
-
-// |C[p][i]| of the orthonormal DCT-III (IDCT) of length b, rounded up to f32
-template <int B>
-struct AbsIdct;
-template <>
-struct AbsIdct<8> {
-    static constexpr float m[8][8] = {
-        {3.535534143e-01f, 4.903926551e-01f, 4.619397819e-01f, 4.157348275e-01f, 3.535534143e-01f, 2.777851522e-01f, 1.913417280e-01f, 9.754516929e-02f},
-        {3.535534143e-01f, 4.157348275e-01f, 1.913417280e-01f, 9.754516929e-02f, 3.535534143e-01f, 4.903926551e-01f, 4.619397819e-01f, 2.777851522e-01f},
-        {3.535534143e-01f, 2.777851522e-01f, 1.913417280e-01f, 4.903926551e-01f, 3.535534143e-01f, 9.754516929e-02f, 4.619397819e-01f, 4.157348275e-01f},
-        {3.535534143e-01f, 9.754516929e-02f, 4.619397819e-01f, 2.777851522e-01f, 3.535534143e-01f, 4.157348275e-01f, 1.913417280e-01f, 4.903926551e-01f},
-        {3.535534143e-01f, 9.754516929e-02f, 4.619397819e-01f, 2.777851522e-01f, 3.535534143e-01f, 4.157348275e-01f, 1.913417280e-01f, 4.903926551e-01f},
-        {3.535534143e-01f, 2.777851522e-01f, 1.913417280e-01f, 4.903926551e-01f, 3.535534143e-01f, 9.754516929e-02f, 4.619397819e-01f, 4.157348275e-01f},
-        {3.535534143e-01f, 4.157348275e-01f, 1.913417280e-01f, 9.754516929e-02f, 3.535534143e-01f, 4.903926551e-01f, 4.619397819e-01f, 2.777851522e-01f},
-        {3.535534143e-01f, 4.903926551e-01f, 4.619397819e-01f, 4.157348275e-01f, 3.535534143e-01f, 2.777851522e-01f, 1.913417280e-01f, 9.754516929e-02f},
-    };
-};
-
-template <>
-struct AbsIdct<16> {
-    static constexpr float m[16][16] = {
-        {2.500000298e-01f, 3.518509567e-01f, 3.467600048e-01f, 3.383295238e-01f, 3.266407847e-01f, 3.118062913e-01f, 2.939689159e-01f, 2.733004987e-01f, 2.500000298e-01f, 2.242919058e-01f, 1.964237541e-01f, 1.666639298e-01f, 1.352990419e-01f, 1.026311368e-01f, 6.897485256e-02f, 3.465429693e-02f},
-        {2.500000298e-01f, 3.383295238e-01f, 2.939689159e-01f, 2.242919058e-01f, 1.352990419e-01f, 3.465429693e-02f, 6.897485256e-02f, 1.666639298e-01f, 2.500000298e-01f, 3.118062913e-01f, 3.467600048e-01f, 3.518509567e-01f, 3.266407847e-01f, 2.733004987e-01f, 1.964237541e-01f, 1.026311368e-01f},
-        {2.500000298e-01f, 3.118062913e-01f, 1.964237541e-01f, 3.465429693e-02f, 1.352990419e-01f, 2.733004987e-01f, 3.467600048e-01f, 3.383295238e-01f, 2.500000298e-01f, 1.026311368e-01f, 6.897485256e-02f, 2.242919058e-01f, 3.266407847e-01f, 3.518509567e-01f, 2.939689159e-01f, 1.666639298e-01f},
-        {2.500000298e-01f, 2.733004987e-01f, 6.897485256e-02f, 1.666639298e-01f, 3.266407847e-01f, 3.383295238e-01f, 1.964237541e-01f, 3.465429693e-02f, 2.500000298e-01f, 3.518509567e-01f, 2.939689159e-01f, 1.026311368e-01f, 1.352990419e-01f, 3.118062913e-01f, 3.467600048e-01f, 2.242919058e-01f},
-        {2.500000298e-01f, 2.242919058e-01f, 6.897485256e-02f, 3.118062913e-01f, 3.266407847e-01f, 1.026311368e-01f, 1.964237541e-01f, 3.518509567e-01f, 2.500000298e-01f, 3.465429693e-02f, 2.939689159e-01f, 3.383295238e-01f, 1.352990419e-01f, 1.666639298e-01f, 3.467600048e-01f, 2.733004987e-01f},
-        {2.500000298e-01f, 1.666639298e-01f, 1.964237541e-01f, 3.518509567e-01f, 1.352990419e-01f, 2.242919058e-01f, 3.467600048e-01f, 1.026311368e-01f, 2.500000298e-01f, 3.383295238e-01f, 6.897485256e-02f, 2.733004987e-01f, 3.266407847e-01f, 3.465429693e-02f, 2.939689159e-01f, 3.118062913e-01f},
-        {2.500000298e-01f, 1.026311368e-01f, 2.939689159e-01f, 2.733004987e-01f, 1.352990419e-01f, 3.518509567e-01f, 6.897485256e-02f, 3.118062913e-01f, 2.500000298e-01f, 1.666639298e-01f, 3.467600048e-01f, 3.465429693e-02f, 3.266407847e-01f, 2.242919058e-01f, 1.964237541e-01f, 3.383295238e-01f},
-        {2.500000298e-01f, 3.465429693e-02f, 3.467600048e-01f, 1.026311368e-01f, 3.266407847e-01f, 1.666639298e-01f, 2.939689159e-01f, 2.242919058e-01f, 2.500000298e-01f, 2.733004987e-01f, 1.964237541e-01f, 3.118062913e-01f, 1.352990419e-01f, 3.383295238e-01f, 6.897485256e-02f, 3.518509567e-01f},
-        {2.500000298e-01f, 3.465429693e-02f, 3.467600048e-01f, 1.026311368e-01f, 3.266407847e-01f, 1.666639298e-01f, 2.939689159e-01f, 2.242919058e-01f, 2.500000298e-01f, 2.733004987e-01f, 1.964237541e-01f, 3.118062913e-01f, 1.352990419e-01f, 3.383295238e-01f, 6.897485256e-02f, 3.518509567e-01f},
-        {2.500000298e-01f, 1.026311368e-01f, 2.939689159e-01f, 2.733004987e-01f, 1.352990419e-01f, 3.518509567e-01f, 6.897485256e-02f, 3.118062913e-01f, 2.500000298e-01f, 1.666639298e-01f, 3.467600048e-01f, 3.465429693e-02f, 3.266407847e-01f, 2.242919058e-01f, 1.964237541e-01f, 3.383295238e-01f},
-        {2.500000298e-01f, 1.666639298e-01f, 1.964237541e-01f, 3.518509567e-01f, 1.352990419e-01f, 2.242919058e-01f, 3.467600048e-01f, 1.026311368e-01f, 2.500000298e-01f, 3.383295238e-01f, 6.897485256e-02f, 2.733004987e-01f, 3.266407847e-01f, 3.465429693e-02f, 2.939689159e-01f, 3.118062913e-01f},
-        {2.500000298e-01f, 2.242919058e-01f, 6.897485256e-02f, 3.118062913e-01f, 3.266407847e-01f, 1.026311368e-01f, 1.964237541e-01f, 3.518509567e-01f, 2.500000298e-01f, 3.465429693e-02f, 2.939689159e-01f, 3.383295238e-01f, 1.352990419e-01f, 1.666639298e-01f, 3.467600048e-01f, 2.733004987e-01f},
-        {2.500000298e-01f, 2.733004987e-01f, 6.897485256e-02f, 1.666639298e-01f, 3.266407847e-01f, 3.383295238e-01f, 1.964237541e-01f, 3.465429693e-02f, 2.500000298e-01f, 3.518509567e-01f, 2.939689159e-01f, 1.026311368e-01f, 1.352990419e-01f, 3.118062913e-01f, 3.467600048e-01f, 2.242919058e-01f},
-        {2.500000298e-01f, 3.118062913e-01f, 1.964237541e-01f, 3.465429693e-02f, 1.352990419e-01f, 2.733004987e-01f, 3.467600048e-01f, 3.383295238e-01f, 2.500000298e-01f, 1.026311368e-01f, 6.897485256e-02f, 2.242919058e-01f, 3.266407847e-01f, 3.518509567e-01f, 2.939689159e-01f, 1.666639298e-01f},
-        {2.500000298e-01f, 3.383295238e-01f, 2.939689159e-01f, 2.242919058e-01f, 1.352990419e-01f, 3.465429693e-02f, 6.897485256e-02f, 1.666639298e-01f, 2.500000298e-01f, 3.118062913e-01f, 3.467600048e-01f, 3.518509567e-01f, 3.266407847e-01f, 2.733004987e-01f, 1.964237541e-01f, 1.026311368e-01f},
-        {2.500000298e-01f, 3.518509567e-01f, 3.467600048e-01f, 3.383295238e-01f, 3.266407847e-01f, 3.118062913e-01f, 2.939689159e-01f, 2.733004987e-01f, 2.500000298e-01f, 2.242919058e-01f, 1.964237541e-01f, 1.666639298e-01f, 1.352990419e-01f, 1.026311368e-01f, 6.897485256e-02f, 3.465429693e-02f},
-    };
-};
+// the list passes of the other sizes exist for this route only (the hybrid route's strip pass
+// there runs every block to the end, kDeferMax<b> = 0): instantiated in tmfwm_rank1_lists.hip
+extern template __global__ void embed_kernel<4, true>(EmbedArgs);
+extern template __global__ void embed_kernel<6, true>(EmbedArgs);
+extern template __global__ void embed_kernel<10, true>(EmbedArgs);
+extern template __global__ void embed_kernel<12, true>(EmbedArgs);
+extern template __global__ void embed_kernel<14, true>(EmbedArgs);
+extern template __global__ void embed_kernel<16, true>(EmbedArgs);
 
 constexpr int kRank1Iters = 4;  // f64 power steps before the a-posteriori test
 
@@ -86,10 +53,9 @@ TMF_DEVI float row_value(const float (&own)[kRows<B, L>])
 }
 
 template <int B>
-__global__ __launch_bounds__(64, B == 8 ? 3 : 2) void embed_rank1_kernel(EmbedArgs a)
+__global__ __launch_bounds__(64, B <= 8 ? 3 : 2) void embed_rank1_kernel(EmbedArgs a)
 {
     constexpr int L = Geo<B>::L, R = Geo<B>::R, BPW = Geo<B>::BPW, LD = B + 1, NW = Geo<B>::NW;
-    static_assert(B == 8 || B == 16, "the rank-1 pre-pass is built for b = 8 and 16");
     constexpr double u53 = 1.1102230246251565e-16;  // 2^-53
     constexpr float u24 = 5.9604644775390625e-08f;  // 2^-24
     __shared__ float lds[BPW * B * LD];
@@ -216,15 +182,20 @@ __global__ __launch_bounds__(64, B == 8 ? 3 : 2) void embed_rank1_kernel(EmbedAr
 #pragma unroll
         for (int j = 0; j < B; ++j) x[r][j] = (float)__builtin_fma(cw * uu[r], v[j], xd[r][j]);
 
-    // eps_Y = k1 (|C| a)_p (|C| b)_q + k2 (|C| u')_p (|C| v')_q + k3 (|C| 1)_p (|C| 1)_q
+    // eps_Y (tools/exp/idct_bound.py): |M_ref - M_fast| <= dM = al a b^T + be u' v'^T + ga 1 1^T and
+    // |M_ref|, |M_fast| <= Mb = (1 + al) a b^T + (|c| + be) u' v'^T + ga 1 1^T; the f32 IDCT is
+    // IDCT_fl(M) = C' M C'^T + R, |R| <= u (E |M| |C'|^T + |C'| |M| E^T) + u^2 E |M| E^T (C' its exact
+    // map, E its first-order rounding bound: IdctBound<B>), so with d_t, m_t the weights above,
+    //   eps_Y = sum_t d_t (|C'| x_t)(|C'| y_t)^T + 2 u m_t ((E x_t)(|C'| y_t)^T + (|C'| x_t)(E y_t)^T
+    //           + u (E x_t)(E y_t)^T),
+    // per pixel (p, q): sum_t A_t(p) P_t(q) + EA_t(p) Q_t(q), P_t = d_t B_t + 2 u m_t EB_t,
+    // Q_t = 2 u m_t (B_t + u EB_t), A_t = |C'| x_t, EA_t = E x_t, B_t = |C'| y_t, EB_t = E y_t
+    using Tb = IdctBound<B>;
     const float e = (float)eps_uv * (1.0f + 0x1p-20f);
     const float cabs = (float)__builtin_fabs(cw) * (1.0f + 0x1p-20f), s1f = (float)s1hi * (1.0f + 0x1p-20f);
-    constexpr float gamL = 16.0f * u24 / (1.0f - 16.0f * u24) * (1.0f + 0x1p-20f);
     const float al = 1.01f * (B + 6) * u24, be = 1.01f * ((B + 6) * u24 * cabs + 2.0f * u24 * (s1f + cabs));
     const float ga = 0x1p-40f * s1f + cabs * e * (2.0f + e);
-    const float k1 = 2.0f * (al * (1.0f + 2.0f * gamL) + 2.0f * gamL);
-    const float k2 = 2.0f * (be * (1.0f + 2.0f * gamL) + 2.0f * gamL * cabs);
-    const float k3 = 2.0f * ga * (1.0f + 2.0f * gamL);
+    const float w1 = 2.0f * u24 * (1.0f + al), w2 = 2.0f * u24 * (cabs + be);  // 2 u m_1, 2 u m_2
     float ra[R], ru[R];  // a_i = |D_i,:|^(1/2), u'_i = |u_i| + e on this lane's rows
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -236,20 +207,23 @@ __global__ __launch_bounds__(64, B == 8 ? 3 : 2) void embed_rank1_kernel(EmbedAr
         av[K] = row_value<B, L, K>(ra);
         uv[K] = row_value<B, L, K>(ru);
     });
-    float Bq[B], Vq[B], Sq[B];  // (|C| b)_q, (|C| v')_q, (|C| 1)_q for every column q
+    float P1[B], Q1[B], P2[B], Q2[B];  // terms a b^T and u' v'^T, every column q
 #pragma unroll
     for (int qq = 0; qq < B; ++qq) {
-        float sb = 0.0f, sv = 0.0f, s1 = 0.0f;
+        float sb = 0.0f, eb = 0.0f, sv = 0.0f, ev = 0.0f;
 #pragma unroll
         for (int j = 0; j < B; ++j) {
-            const float cij = AbsIdct<B>::m[qq][j];
-            sb = __builtin_fmaf(cij, __builtin_sqrtf(__builtin_sqrtf((float)cn[j] * (1.0f + 0x1p-20f))) * (1.0f + 0x1p-20f), sb);
-            sv = __builtin_fmaf(cij, (float)__builtin_fabs(v[j]) + e, sv);
-            s1 += cij;
+            const float bj = __builtin_sqrtf(__builtin_sqrtf((float)cn[j] * (1.0f + 0x1p-20f))) * (1.0f + 0x1p-20f);
+            const float vj = (float)__builtin_fabs(v[j]) + e;
+            sb = __builtin_fmaf(Tb::absc[qq][j], bj, sb);
+            eb = __builtin_fmaf(Tb::err[qq][j], bj, eb);
+            sv = __builtin_fmaf(Tb::absc[qq][j], vj, sv);
+            ev = __builtin_fmaf(Tb::err[qq][j], vj, ev);
         }
-        Bq[qq] = sb;
-        Vq[qq] = sv;
-        Sq[qq] = s1;
+        P1[qq] = __builtin_fmaf(al, sb, w1 * eb);
+        Q1[qq] = w1 * __builtin_fmaf(u24, eb, sb);
+        P2[qq] = __builtin_fmaf(be, sv, w2 * ev);
+        Q2[qq] = w2 * __builtin_fmaf(u24, ev, sv);
     }
 
     dct2d_rows_layout<B, true>(x, tile, q);  // :204, Y_fast
@@ -259,18 +233,24 @@ __global__ __launch_bounds__(64, B == 8 ? 3 : 2) void embed_rank1_kernel(EmbedAr
     uint32_t outw[R][NW];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        float Ap = 0.0f, Up = 0.0f, Sp = 0.0f;
-        // (|C| a)_p, (|C| u')_p, (|C| 1)_p: the IDCT matrix row of this pixel row (p = q R + r is
-        // lane-dependent: the entries come from the table by a select over the L lanes' rows)
+        float Ap = 0.0f, EAp = 0.0f, Up = 0.0f, EUp = 0.0f, Sp = 0.0f, ESp = 0.0f;
+        // A_t(p), EA_t(p): the tables' row of this pixel row (p = q R + r is lane-dependent: the
+        // entries come from the tables by a select over the L lanes' rows)
         static_for<B>([&](auto I) {
-            float cpi = AbsIdct<B>::m[r][I];
-            static_for<L - 1>([&](auto Q1) {
-                constexpr int QQ = Q1 + 1;
-                if (QQ * R + r < B) cpi = q == QQ ? AbsIdct<B>::m[(QQ * R + r) % B][I] : cpi;
+            float cpi = Tb::absc[r][I], epi = Tb::err[r][I];
+            static_for<L - 1>([&](auto Q1_) {
+                constexpr int QQ = Q1_ + 1;
+                if (QQ * R + r < B) {
+                    cpi = q == QQ ? Tb::absc[(QQ * R + r) % B][I] : cpi;
+                    epi = q == QQ ? Tb::err[(QQ * R + r) % B][I] : epi;
+                }
             });
             Ap = __builtin_fmaf(cpi, av[I], Ap);
+            EAp = __builtin_fmaf(epi, av[I], EAp);
             Up = __builtin_fmaf(cpi, uv[I], Up);
+            EUp = __builtin_fmaf(epi, uv[I], EUp);
             Sp += cpi;
+            ESp += epi;
         });
         uint32_t words[NW];
 #pragma unroll
@@ -281,7 +261,15 @@ __global__ __launch_bounds__(64, B == 8 ? 3 : 2) void embed_rank1_kernel(EmbedAr
 #pragma unroll
         for (int c = 0; c < B; ++c) {
             const float y = x[r][c];
-            const float ey = (k1 * Ap * Bq[c] + k2 * Up * Vq[c] + k3 * Sp * Sq[c]) * (1.0f + 0x1p-16f) +
+            // the ones term's column factors are compile-time sums of the tables
+            float B3 = 0.0f, EB3 = 0.0f;
+#pragma unroll
+            for (int j = 0; j < B; ++j) {
+                B3 += Tb::absc[c][j];
+                EB3 += Tb::err[c][j];
+            }
+            const float t3 = Sp * __builtin_fmaf(2.0f * u24, EB3, B3) + ESp * (2.0f * u24) * __builtin_fmaf(u24, EB3, B3);
+            const float ey = (Ap * P1[c] + EAp * Q1[c] + Up * P2[c] + EUp * Q2[c] + ga * t3) * (1.0f + 0x1p-16f) +
                              __builtin_fabsf(y) * 0x1p-22f + 0x1p-40f;
             float cbs, crs;
             const uint32_t R0 = byte_at(words, 3 * c), G0 = byte_at(words, 3 * c + 1), B0 = byte_at(words, 3 * c + 2);
@@ -341,9 +329,9 @@ static hipError_t launch_rank1_b(EmbedArgs a, hipStream_t st)
     return hipGetLastError();
 }
 
-bool rank1_block(int block) { return block == 8 || block == 16; }
+bool rank1_block(int block) { return block >= 4 && block <= 16 && block % 2 == 0; }
 
-// The rank-1 pre-pass at b = 8 / 16 over every block, then the edge pixels.  TMFWM_ROUTE_RANK1
+// The rank-1 pre-pass over every block (every slider size, b = 4..16 even), then the edge pixels.  TMFWM_ROUTE_RANK1
 // (a.slow_list set): the list pass (embed_kernel<b, true>: the full hybrid route) over the blocks
 // it left; TMFWM_ROUTE_RANK1_REFERENCE (no slow list): those blocks went to the dgesdd-route list.
 // Either way the caller runs the dgesdd-route fixup next.  The caller handles other block sizes.
@@ -351,7 +339,16 @@ hipError_t launch_embed_rank1(EmbedArgs a, hipStream_t st)
 {
     if (!rank1_block(a.block)) return hipErrorInvalidValue;
     if (a.nbh > 0 && a.nbw > 0) {
-        const hipError_t e = a.block == 8 ? launch_rank1_b<8>(a, st) : launch_rank1_b<16>(a, st);
+        hipError_t e = hipErrorInvalidValue;
+        switch (a.block) {
+        case 4: e = launch_rank1_b<4>(a, st); break;
+        case 6: e = launch_rank1_b<6>(a, st); break;
+        case 8: e = launch_rank1_b<8>(a, st); break;
+        case 10: e = launch_rank1_b<10>(a, st); break;
+        case 12: e = launch_rank1_b<12>(a, st); break;
+        case 14: e = launch_rank1_b<14>(a, st); break;
+        case 16: e = launch_rank1_b<16>(a, st); break;
+        }
         if (e != hipSuccess) return e;
     }
     return launch_edges(a.src, a.dst, a.nframes, a.H, a.W, a.frame_stride, a.block, st);

@@ -37,6 +37,11 @@ F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -
 /opt/rocm/bin/hipcc $F -c "$K/tmfwm_kernels.hip" -o "$T/k.o" &
 /opt/rocm/bin/hipcc $F -mllvm -amdgpu-sched-strategy=${E8SCHED:-max-ilp} -c "$K/tmfwm_embed8.hip" -o "$T/e8.o" &
 /opt/rocm/bin/hipcc $F -c "$K/tmfwm_rank1.hip" -o "$T/r1.o" &
+R1L=
+if [ -f "$K/tmfwm_rank1_lists.hip" ]; then  # (before round 6's last builds: in tmfwm_rank1.hip)
+  R1L="$T/r1l.o"
+  /opt/rocm/bin/hipcc $F -c "$K/tmfwm_rank1_lists.hip" -o "$T/r1l.o" &
+fi
 FB="$C/tmfwm_fallback.o $C/tmfwm_fixup4.o $C/tmfwm_fixup6.o $C/tmfwm_fixup8.o $C/tmfwm_fixup10.o $C/tmfwm_fixup12.o $C/tmfwm_fixup14.o $C/tmfwm_fixup16.o"
 if [ "${FALLBACK:-0}" = "1" ]; then
   FB="$T/fb.o"
@@ -48,7 +53,7 @@ if [ "${FALLBACK:-0}" = "1" ]; then
 fi
 wait
 mkdir -p "$ROOT/ab"
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$ROOT/ab/libtmfwm_$NAME.so" "$T/k.o" "$T/e8.o" "$T/r1.o" \
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$ROOT/ab/libtmfwm_$NAME.so" "$T/k.o" "$T/e8.o" "$T/r1.o" $R1L \
     "$C/tmfwm_capi.o" "$C/tmfwm_multi.o" "$C/tmfwm_qr.o" "$C/tmfwm_tile.o" "$C/tmfwm_pixels.o" $FB -fopenmp -ldl -lpthread
 rm -rf "$T"
 echo "ab/libtmfwm_$NAME.so"

@@ -30,6 +30,7 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from oracle import oracle as O  # noqa: E402
+import idct_bound as IB  # noqa: E402
 from lapack_path import _blocks, _unblocks, photo_cover  # noqa: E402
 from cert_study import lp_f64  # noqa: E402
 
@@ -155,18 +156,23 @@ def certify_rank1(cov, tile, b, alpha=0.1, iters=4):
     al = 1.01 * (b + 6) * U32
     be = 1.01 * ((b + 6) * U32 * ca + 2 * U32 * (s1hi + ca))
     ga = 2.0**-40 * s1hi + ca * e * (2 + e)
-    gL = 16 * U32 / (1 - 16 * U32)
-    k1, k2, k3 = 2 * (al * (1 + 2 * gL) + 2 * gL), 2 * (be * (1 + 2 * gL) + 2 * gL * ca), 2 * ga * (1 + 2 * gL)
-    k1 = np.broadcast_to(np.asarray(k1, np.float64), (n,))
-    C = np.abs(dct_matrix(b)).T  # the IDCT matrix |C|[p][i]
+    # |M_ref - M_fast| <= dM = al a b^T + be u' v'^T + ga 1 1^T, and both |M_ref|, |M_fast| <= Mb =
+    # (1 + al) a b^T + (|c| + be) u' v'^T + ga 1 1^T; through the f32 IDCT (tools/exp/idct_bound.py:
+    # IDCT_fl(M) = C' M C'^T + R, |R| <= u (E |M| |C'|^T + |C'| |M| E^T) + u^2 E |M| E^T):
+    # eps_Y = |C'| dM |C'|^T + 2 (u (E Mb |C'|^T + |C'| Mb E^T) + u^2 E Mb E^T), every term rank one
+    absc, err = (np.array(t) for t in IB.tables(b))  # [p][i]
     a_ = np.sqrt(np.sqrt(rn))
     b_ = np.sqrt(np.sqrt(cn))
     up, vp = np.abs(u) + e[:, None], np.abs(v) + e[:, None]
-    A, Bq = a_ @ C.T, b_ @ C.T
-    Up, Vq = up @ C.T, vp @ C.T
-    S = C.sum(axis=1)
-    epsY = (k1[:, None, None] * A[:, :, None] * Bq[:, None, :] + k2[:, None, None] * Up[:, :, None] * Vq[:, None, :]
-            + k3[:, None, None] * S[None, :, None] * S[None, None, :]) * (1 + 2.0**-16) + np.abs(Yf) * 2.0**-22 + 2.0**-40
+    one = np.ones((n, b))
+    epsY = np.zeros((n, b, b))
+    for x_, y_, d_, m_ in ((a_, b_, np.full(n, al), np.full(n, 1 + al)), (up, vp, be, ca + be), (one, one, ga, ga)):
+        A, EA = x_ @ absc.T, x_ @ err.T
+        Bq, EB = y_ @ absc.T, y_ @ err.T
+        epsY += d_[:, None, None] * A[:, :, None] * Bq[:, None, :]
+        epsY += (2 * U32 * m_)[:, None, None] * (EA[:, :, None] * Bq[:, None, :] + A[:, :, None] * EB[:, None, :]
+                                                 + U32 * EA[:, :, None] * EB[:, None, :])
+    epsY = epsY * (1 + 2.0**-16) + np.abs(Yf) * 2.0**-22 + 2.0**-40
     Yp = _unblocks(Yf, nbh, nbw, b).astype(np.float64)
     Ep = _unblocks(epsY, nbh, nbw, b)
     cbp = (ycc[: nbh * b, : nbw * b, 1] - np.float32(0.5)).astype(np.float64)

@@ -22,6 +22,9 @@ def main():
     out = subprocess.run(cmd, cwd=CSRC, capture_output=True, text=True).stderr
     cmd8 = [c if c != "tmfwm_kernels.hip" else "tmfwm_embed8.hip" for c in cmd] + ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]
     out += subprocess.run(cmd8, cwd=CSRC, capture_output=True, text=True).stderr
+    for tu in ("tmfwm_rank1.hip", "tmfwm_rank1_lists.hip"):
+        out += subprocess.run([c if c != "tmfwm_kernels.hip" else tu for c in cmd], cwd=CSRC, capture_output=True,
+                              text=True).stderr
     rows, cur = [], None
     for line in out.splitlines():
         m = re.search(r"remark: +(Function Name|VGPRs|AGPRs|ScratchSize \[bytes/lane\]|Occupancy \[waves/SIMD\]|VGPRs Spill|LDS Size \[bytes/block\]): (\S+)", line)
