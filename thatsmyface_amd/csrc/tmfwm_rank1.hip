@@ -11,16 +11,18 @@
 //       pair (e = eps_uv, below), alpha' = 1.01 (b + 6) 2^-24 (the b fmaf roundings of the chain,
 //       the 4 factor roundings, f32(M_fast)), beta' = 1.01 ((b + 6) 2^-24 |c| + 2^-23 (s1 + |c|))
 //       (S[0]'s and S'[0]'s f32 roundings), gamma' = 2^-40 s1 (LAPACK's residual |U S V^T - D|,
-//       8192 units of 2^-53 s1) + |c| e (2 + e);
-//   eps_Y = 2 |C| (dM + 2 gamma_16 (G + |c| P + dM)) |C|^T  (|C| the ortho IDCT matrix rounded
-//     up; both IDCTs' roundings, pocketfft's depth allowance 16) -- rank-three, so per pixel three
-//     products of |C|-transformed vectors;
+//       8192 units of 2^-53 s1, 84 times the worst measured) + |c| e (2 + e);
+//   eps_Y = |C'| dM |C'|^T + 2 (u (E Mb |C'|^T + |C'| Mb E^T) + u^2 E Mb E^T),  Mb = G + |c| P + dM
+//     bounding both |M_ref| and |M_fast|; C' the f32 IDCT's exact linear map, E the first-order
+//     bound of its roundings per input (|IDCT_fl(x) - C' x| <= u E |x|), both from a transcription
+//     of the op sequence (tools/exp/idct_bound.py -> tmfwm_idct_bounds.h, every slider length) --
+//     rank-three, so per pixel six products of |C'|- and E-transformed vectors;
 // and keeps a block's bytes when every channel gives the same byte at Y_fast - eps_Y and
 // Y_fast + eps_Y (each channel is monotone in Y).  Top pair: with v the iterate, rho = |Dv|^2 /
 // |v|^2, r = D^T D v - rho v and F = |D|_F^2, the extract's Kato-Temple margins (sigma1_certified)
 // give lambda_1 in [rho, rho + |r|^2 / gap], gap = 2 rho - F, and Davis-Kahan sin(v, v1) <=
 // |r| / (|v| gap); u = D v / |D v| is no further from u1; LAPACK's own top pair is within
-// 1024 2^-53 s1 / (s1 - s2) (ten times the worst any triplet showed in the K study, 3.5; the
+// 1024 2^-53 s1 / (s1 - s2) (6.4 times the worst measured, tools/exp/lapack_bounds.py; the
 // pass requires e <= 2^-30, so e's share of the bound is below 2^-29 |c| whatever that constant).
 // A block that fails any test (no spectral gap, an undecided byte) writes nothing and goes to the
 // slow list, whose list pass (embed_kernel<b, true>) redoes it on the full hybrid route -- Jacobi
