@@ -1162,3 +1162,23 @@ def test_multi_entry_points_reference_route(dev):
         ref = O.embed_frame(host[f], t, b, 0.1, route="lapack")
         assert np.array_equal(out[f], ref), f
         assert np.array_equal(ext[f], O.extract_frame(ref, host[f], b, 0.1, route="lapack")), f
+
+
+@pytest.mark.parametrize("route", ["rank1", "rank1_reference"])
+def test_multi_entry_points_rank1_routes(dev, route):
+    """tmfwm_embed_multi_route / tmfwm_extract_multi_route on the rank-1 routes (ABI 10), two logical
+    shards on device 0, b = 8 and 12, camera-like frames: the oracle's dgesdd route for every frame."""
+    from lapack_path import photo_cover
+
+    from thatsmyface_amd import multi
+
+    H, W, n = 136, 232, 3
+    host = np.stack([photo_cover(H, W, 70 + i) for i in range(n)])
+    for b in (8, 12):
+        t = _u8(71 + b, (H // b, W // b))
+        out = multi.embed_multi(host, t, b, 0.1, devices=[0, 0], route=route)
+        ext = multi.extract_multi(out, host, b, 0.1, devices=[0, 0], route=route)
+        for f in range(n):
+            ref = O.embed_frame(host[f], t, b, 0.1, route="lapack")
+            assert np.array_equal(out[f], ref), (b, f)
+            assert np.array_equal(ext[f], O.extract_frame(ref, host[f], b, 0.1, route="lapack")), (b, f)

@@ -34,7 +34,7 @@ def embed_multi(frames: np.ndarray, wm_tile: np.ndarray, block: int = 8, alpha: 
                 stats: dict | None = None, route: str = "hybrid") -> np.ndarray:
     """Embed one tile into every frame, frames sharded over `devices` (default: every
     visible GPU; repeat a device for logical shards).  stats receives "lapack_blocks";
-    route as batch.embed_batch ("hybrid" or "reference")."""
+    route as batch.embed_batch ("hybrid", "reference", "rank1" or "rank1_reference")."""
     frames = _frames(frames, "frames")
     n, h, w, _ = frames.shape
     if block not in SUPPORTED_BLOCK_SIZES:
