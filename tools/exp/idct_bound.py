@@ -308,8 +308,8 @@ def tables(n):
 
 def emit(path):
     out = ["// Generated by tools/exp/idct_bound.py --emit: do not edit.  The rank-1 pre-pass's IDCT",
-           "// tables (DESIGN.md 5): kAbsC[p][i] >= |C'[p][i]|, C' the exact linear map of the f32 IDCT",
-           "// (pocketfft's DCT-III, ortho) with its f32 constants; kErr[p][i] >= E[p][i], the first-order",
+           "// tables (DESIGN.md 5): absc[p][i] >= |C'[p][i]|, C' the exact linear map of the f32 IDCT",
+           "// (pocketfft's DCT-III, ortho) with its f32 constants; err[p][i] >= E[p][i], the first-order",
            "// rounding bound |IDCT_fl(x)_p - (C' x)_p| <= 2^-24 sum_i E[p][i] |x_i| of that op sequence.",
            "#pragma once", "", "namespace tmf {", "", "template <int B>", "struct IdctBound;"]
     for n in (4, 6, 8, 10, 12, 14, 16):
