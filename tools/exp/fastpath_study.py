@@ -13,7 +13,10 @@ and a per-pixel bound eps_Y >= |Y_ref - Y_fast|:
     residual |U S V^T - D|, K_A = 1024); eps_uv bounds the top pair's disagreement (K 2^-53 s1/gap1);
     the (b+5) u counts the b fmaf roundings of the chain, 4 factor roundings and the f32(M_fast);
   eps_Y = kappa |C| (dM + 2 gamma_L (|M_fast| + dM)) |C|^T   (linear part + both IDCT roundings;
-    |C| the exact ortho DCT-III matrix, kappa = 2, L = 16 as the pocketfft depth allowance).
+    |C| the exact ortho DCT-III matrix, kappa = 2, L = 16 as the pocketfft depth allowance) --
+    round 4's allowance, kept here as that study ran; the shipped pre-pass and certify_rank1 below
+    use the IDCT rounding bound derived from the op sequence (tools/exp/idct_bound.py), which this
+    allowance undercuts where |C| is small.
 A channel byte is certain when the colour inverse (monotone in Y, slope 1) gives the same byte
 for every Y in [Y_fast - eps_Y, Y_fast + eps_Y] (f32 rounding slack included); a block is
 certified when all its bytes are.  Reported: certified fraction, and that every certified
