@@ -85,6 +85,8 @@ def tu_kernels(obj):
 
 
 def main():
+    if len(sys.argv) < 3 or sys.argv[1].startswith("-"):
+        sys.exit("usage: kernel_ids.py OUT.json OBJ.o [OBJ.o ...]")
     out, objs = sys.argv[1], sys.argv[2:]
     kernels, tus = {}, {}
     for o in objs:
